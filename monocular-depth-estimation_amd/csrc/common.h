@@ -1,0 +1,91 @@
+// Shared helpers for the mdemi gfx950 kernels: error reporting for the C ABI,
+// wave64 reductions, vector types.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include "mdemi.h"
+
+namespace mdemi {
+
+void set_error(const char* fmt, ...);
+
+// Launch-status check used by every entry point after its last launch.
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return MDEMI_ELAUNCH;
+  }
+  return MDEMI_OK;
+}
+
+#define MDEMI_REQUIRE(cond, ...)            \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::mdemi::set_error(__VA_ARGS__);      \
+      return MDEMI_EINVAL;                  \
+    }                                       \
+  } while (0)
+
+// ---- wave64 reductions (DPP/shuffle through __shfl_xor over all 64 lanes) ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block reduction for blockDim.x == NT (multiple of 64); `red` holds NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__device__ __forceinline__ float apply_act(int act, float v) {
+  switch (act) {
+    case MDEMI_ACT_GELU: return gelu_f(v);
+    case MDEMI_ACT_RELU: return v > 0.f ? v : 0.f;
+    case MDEMI_ACT_LEAKY: return v > 0.f ? v : 0.01f * v;
+    case MDEMI_ACT_SIGMOID: return sigmoid_f(v);
+    default: return v;
+  }
+}
+// derivative of act expressed through the pre-activation x (and/or output y)
+__device__ __forceinline__ float act_grad(int act, float x, float y) {
+  switch (act) {
+    case MDEMI_ACT_GELU: return gelu_grad_f(x);
+    case MDEMI_ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    case MDEMI_ACT_LEAKY: return x > 0.f ? 1.f : 0.01f;
+    case MDEMI_ACT_SIGMOID: return y * (1.f - y);
+    default: return 1.f;
+  }
+}
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace mdemi

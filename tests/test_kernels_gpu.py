@@ -1,0 +1,342 @@
+"""Kernel-level numerics: every libmdemi kernel against a plain PyTorch fp64
+CPU reference of the same op (forward and backward).  Tolerances are stated
+per test; fp32 kernels are held to ~1e-5 relative on O(1) data."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(*shape, generator=g, dtype=torch.float64) * 2 - 1) * scale
+
+
+def close(a, b, rtol=2e-5, atol=2e-5):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item()
+    assert err <= atol + rtol * ref, f"max|diff|={err:.3e} max|ref|={ref:.3e}"
+
+
+@pytest.fixture(scope="module")
+def mf():
+    from mdemi import functional as mf
+    from mdemi import _lib
+    _lib.load()
+    return mf
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 16), (300, 200, 70), (1, 5, 3), (517, 384, 192), (64, 1536, 384)])
+def test_linear_fwd_bwd(mf, M, N, K):
+    x, w, b = rnd(M, K, seed=1), rnd(N, K, seed=2, scale=0.1), rnd(N, seed=3)
+    res = rnd(M, N, seed=4)
+    dy = rnd(M, N, seed=5)
+    xr, wr, br, rr = [t.clone().requires_grad_() for t in (x, w, b, res)]
+    yr = F.linear(xr, wr, br) + rr
+    yr.backward(dy)
+    xg, wg, bg, rg = [t.float().to(DEV).requires_grad_() for t in (x, w, b, res)]
+    yg = mf.linear(xg, wg, bg, residual=rg)
+    yg.backward(dy.float().to(DEV))
+    tol = dict(rtol=1e-5 * max(1, math.sqrt(K)), atol=1e-5)
+    close(yg, yr, **tol)
+    close(xg.grad, xr.grad, rtol=1e-5 * math.sqrt(N), atol=1e-5)
+    close(wg.grad, wr.grad, rtol=1e-5 * math.sqrt(M), atol=1e-5)
+    close(bg.grad, br.grad, rtol=1e-5 * math.sqrt(M), atol=1e-5)
+    close(rg.grad, rr.grad)
+
+
+def test_linear_gelu_on_load(mf):
+    M, K, N = 333, 96, 48
+    h, w, b = rnd(M, K, seed=6, scale=3), rnd(N, K, seed=7, scale=0.2), rnd(N, seed=8)
+    dy = rnd(M, N, seed=9)
+    hr, wr, br = [t.clone().requires_grad_() for t in (h, w, b)]
+    yr = F.linear(F.gelu(hr), wr, br)
+    yr.backward(dy)
+    hg, wg, bg = [t.float().to(DEV).requires_grad_() for t in (h, w, b)]
+    yg = mf.linear(hg, wg, bg, in_gelu=True)
+    yg.backward(dy.float().to(DEV))
+    close(yg, yr, rtol=1e-4)
+    close(hg.grad, hr.grad, rtol=1e-4)
+    close(wg.grad, wr.grad, rtol=1e-4)
+
+
+def test_gemm_splitk_and_batch(mf):
+    from mdemi import _lib as L
+    B, M, N, K = 3, 70, 90, 1000
+    a, b = rnd(B, M, K, seed=10), rnd(B, N, K, seed=11)
+    ref = torch.einsum("bmk,bnk->bmn", a, b)
+    ag, bg = a.float().to(DEV), b.float().to(DEV)
+    for split in (1, 7):
+        c = torch.empty(B, M, N, device=DEV)
+        mf.gemm(ag, bg, c, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG, batch=B,
+                a_bstride=M * K, b_bstride=N * K, c_bstride=M * N, split_k=split)
+        close(c, ref, rtol=1e-4)
+
+
+@pytest.mark.parametrize("cin,cout,k,s,p,hw", [(8, 16, 3, 1, 1, (9, 13)), (64, 32, 3, 1, 1, (15, 20)),
+                                              (12, 8, 1, 1, 0, (7, 5)), (16, 24, 3, 2, 1, (11, 10))])
+def test_conv2d_nhwc(mf, cin, cout, k, s, p, hw):
+    n = 2
+    x, w, b = rnd(n, cin, *hw, seed=12), rnd(cout, cin, k, k, seed=13, scale=0.2), rnd(cout, seed=14)
+    xr, wr, br = [t.clone().requires_grad_() for t in (x, w, b)]
+    yr = F.conv2d(xr, wr, br, stride=s, padding=p)
+    dy = rnd(*yr.shape, seed=15)
+    yr.backward(dy)
+    xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV).requires_grad_()
+    wg, bg = w.float().to(DEV).requires_grad_(), b.float().to(DEV).requires_grad_()
+    yg = mf.conv2d_nhwc(xg, wg, bg, stride=s, pad=p)
+    close(yg.permute(0, 3, 1, 2), yr, rtol=1e-4)
+    need_dx = s == 1
+    if not need_dx:
+        xg = xg.detach()
+        yg = mf.conv2d_nhwc(xg, wg, bg, stride=s, pad=p)
+    yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+    if need_dx:
+        close(xg.grad.permute(0, 3, 1, 2), xr.grad, rtol=1e-4)
+    close(wg.grad, wr.grad, rtol=1e-4)
+    close(bg.grad, br.grad, rtol=1e-4)
+
+
+@pytest.mark.parametrize("rows,C", [(1000, 192), (37, 1536), (5, 3072), (100, 64)])
+def test_layernorm(mf, rows, C):
+    x, g, b = rnd(rows, C, seed=16, scale=2) + 0.5, rnd(C, seed=17), rnd(C, seed=18)
+    dy = rnd(rows, C, seed=19)
+    xr, gr, br = [t.clone().requires_grad_() for t in (x, g, b)]
+    yr = F.layer_norm(xr, (C,), gr, br, 1e-5)
+    yr.backward(dy)
+    xg, gg, bg = [t.float().to(DEV).requires_grad_() for t in (x, g, b)]
+    yg = mf.layer_norm(xg, gg, bg, 1e-5)
+    yg.backward(dy.float().to(DEV))
+    close(yg, yr, rtol=1e-5)
+    close(xg.grad, xr.grad, rtol=1e-4)
+    close(gg.grad, gr.grad, rtol=1e-4)
+    close(bg.grad, br.grad, rtol=1e-4)
+
+
+def _ref_window_attn(qk, qk_bias, v, v_bias, rpb, B, H, W, heads, ws, shift, scale, C, v_off):
+    """Direct restatement of WindowAttention + pad/roll/partition (swin_transformer.py:112-240)."""
+    hd = C // heads
+    rows = B * H * W
+    q = qk[:, :C]
+    k = qk[:, C:2 * C]
+    vv = v[:, v_off:v_off + C]
+    Hp, Wp = -(-H // ws) * ws, -(-W // ws) * ws
+
+    def grid(t, pad):
+        t = t.view(B, H, W, C)
+        full = (pad.view(1, 1, 1, C) if pad is not None else torch.zeros(1, 1, 1, C, dtype=t.dtype)).expand(
+            B, Hp, Wp, C).clone()
+        full[:, :H, :W] = t
+        if shift:
+            full = torch.roll(full, (-shift, -shift), (1, 2))
+        return full.view(B, Hp // ws, ws, Wp // ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(-1, ws * ws, C)
+
+    qw = grid(q, qk_bias[:C] if qk_bias is not None else None)
+    kw = grid(k, qk_bias[C:2 * C] if qk_bias is not None else None)
+    vw = grid(vv, v_bias[v_off:v_off + C] if v_bias is not None else None)
+    nW = qw.shape[0] // B
+    qh = qw.view(-1, ws * ws, heads, hd).transpose(1, 2) * scale
+    kh = kw.view(-1, ws * ws, heads, hd).transpose(1, 2)
+    vh = vw.view(-1, ws * ws, heads, hd).transpose(1, 2)
+    attn = qh @ kh.transpose(-2, -1)
+    coords = torch.stack(torch.meshgrid(torch.arange(ws), torch.arange(ws), indexing="ij")).flatten(1)
+    rel = (coords[:, :, None] - coords[:, None, :]).permute(1, 2, 0)
+    idx = (rel[..., 0] + ws - 1) * (2 * ws - 1) + rel[..., 1] + ws - 1
+    attn = attn + rpb[idx.view(-1)].view(ws * ws, ws * ws, heads).permute(2, 0, 1).unsqueeze(0)
+    if shift:
+        img = torch.zeros(1, Hp, Wp, 1, dtype=qk.dtype)
+        cnt = 0
+        for hs in (slice(0, -ws), slice(-ws, -shift), slice(-shift, None)):
+            for wsl in (slice(0, -ws), slice(-ws, -shift), slice(-shift, None)):
+                img[:, hs, wsl, :] = cnt
+                cnt += 1
+        mw = img.view(1, Hp // ws, ws, Wp // ws, ws, 1).permute(0, 1, 3, 2, 4, 5).reshape(-1, ws * ws)
+        mask = mw.unsqueeze(1) - mw.unsqueeze(2)
+        mask = mask.masked_fill(mask != 0, -100.0).masked_fill(mask == 0, 0.0)
+        attn = attn.view(B, nW, heads, ws * ws, ws * ws) + mask.unsqueeze(1).unsqueeze(0)
+        attn = attn.view(-1, heads, ws * ws, ws * ws)
+    attn = attn.softmax(-1)
+    o = (attn @ vh).transpose(1, 2).reshape(-1, ws * ws, C)
+    o = o.view(B, Hp // ws, Wp // ws, ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B, Hp, Wp, C)
+    if shift:
+        o = torch.roll(o, (shift, shift), (1, 2))
+    return o[:, :H, :W].reshape(rows, C)
+
+
+@pytest.mark.parametrize("H,W,shift,swin", [(14, 14, 0, True), (10, 12, 3, True), (9, 16, 3, False),
+                                            (7, 7, 3, True), (15, 20, 0, False)])
+def test_window_attention(mf, H, W, shift, swin):
+    B, heads, C, ws = 2, 2, 64, 7
+    rows = B * H * W
+    scale = (C // heads) ** -0.5
+    rpb = rnd(169, heads, seed=20)
+    if swin:
+        qk = rnd(rows, 3 * C, seed=21)
+        qkb = rnd(3 * C, seed=22)
+        v, vb, v_off = qk, qkb, 2 * C
+    else:
+        qk = rnd(rows, 2 * C, seed=21)
+        qkb = rnd(2 * C, seed=22)
+        v, vb, v_off = rnd(rows, C, seed=23), None, 0
+    dout = rnd(rows, C, seed=24)
+    leaves = [qk, qkb, rpb] + ([] if swin else [v])
+    refs = {id(t): t.clone().requires_grad_() for t in leaves}
+    qk_r, qkb_r, rpb_r = refs[id(qk)], refs[id(qkb)], refs[id(rpb)]
+    v_r = qk_r if swin else refs[id(v)]
+    vb_r = qkb_r if swin else None
+    out_r = _ref_window_attn(qk_r, qkb_r, v_r, vb_r, rpb_r, B, H, W, heads, ws, shift, scale, C, v_off)
+    out_r.backward(dout)
+    g = {k: t.detach().float().to(DEV).requires_grad_() for k, t in refs.items()}
+    qk_g, qkb_g, rpb_g = g[id(qk)], g[id(qkb)], g[id(rpb)]
+    v_g = qk_g if swin else g[id(v)]
+    vb_g = qkb_g if swin else None
+    out_g = mf.window_attention(qk_g, qkb_g, v_g, vb_g, rpb_g, B, H, W, heads, ws, shift, scale, C, v_off)
+    out_g.backward(dout.float().to(DEV))
+    close(out_g, out_r, rtol=1e-4)
+    close(qk_g.grad, qk_r.grad, rtol=1e-4)
+    close(qkb_g.grad, qkb_r.grad, rtol=1e-4)
+    close(rpb_g.grad, rpb_r.grad, rtol=1e-4)
+    if not swin:
+        close(v_g.grad, v_r.grad, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B,K,H,W,softmax", [(2, 256, 24, 32, True), (3, 17, 5, 7, True), (2, 64, 8, 8, False)])
+def test_bin_head(mf, B, K, H, W, softmax):
+    logits = rnd(B, K, H, W, seed=30, scale=4)
+    if not softmax:
+        logits = logits.softmax(1)
+    centers = rnd(B, K, seed=31).abs() * 10
+    dpred = rnd(B, 1, H, W, seed=32)
+    lr, cr = logits.clone().requires_grad_(), centers.clone().requires_grad_()
+    pr = lr.softmax(1) if softmax else lr
+    pred_r = (pr * cr.view(B, K, 1, 1)).sum(1, keepdim=True)
+    pred_r.backward(dpred)
+    lg, cg = logits.float().to(DEV).requires_grad_(), centers.float().to(DEV).requires_grad_()
+    pred_g = mf.bin_head(lg, cg, do_softmax=softmax)
+    pred_g.backward(dpred.float().to(DEV))
+    close(pred_g, pred_r, rtol=1e-5)
+    close(lg.grad, lr.grad, rtol=1e-4, atol=1e-5)
+    close(cg.grad, cr.grad, rtol=1e-4)
+
+
+@pytest.mark.parametrize("per_image,unbiased", [(False, False), (True, False), (True, True)])
+def test_silog(mf, per_image, unbiased):
+    B, H, W = 3, 40, 52
+    gt = rnd(B, 1, H, W, seed=40).abs() * 9 + 0.5
+    gt[:, :, :5] = 0.0  # invalid region
+    pred = rnd(B, 1, H, W, seed=41).abs() * 9 + 0.5
+    alpha, beta, md = 10.0, 0.15, 1e-3
+    pr = pred.clone().requires_grad_()
+
+    def group_loss(p, g):
+        m = g > md
+        d = torch.log(p[m]) - torch.log(g[m])
+        var = d.var() if unbiased else (d * d).mean() - d.mean() ** 2
+        return alpha * torch.sqrt(var + beta * d.mean() ** 2)
+
+    if per_image:
+        lr = torch.stack([group_loss(pr[b], gt[b]) for b in range(B)]).mean()
+    else:
+        lr = group_loss(pr, gt)
+    lr.backward()
+    pg = pred.float().to(DEV).requires_grad_()
+    lg = mf.silog_loss(pg, gt.float().to(DEV), md, alpha, beta, per_image, unbiased)
+    lg.backward()
+    close(lg, lr, rtol=1e-5)
+    close(pg.grad, pr.grad, rtol=1e-3, atol=1e-7)
+
+
+@pytest.mark.parametrize("hw,out,align,sf", [((15, 20), (60, 80), False, 4.0), ((3, 3), (15, 20), False, None),
+                                             ((30, 40), (60, 80), True, None), ((1, 1), (15, 20), False, None),
+                                             ((7, 9), (5, 4), True, None)])
+def test_bilinear(mf, hw, out, align, sf):
+    n, c = 2, 8
+    x = rnd(n, c, *hw, seed=50)
+    xr = x.clone().requires_grad_()
+    if sf is not None:
+        yr = F.interpolate(xr, scale_factor=sf, mode="bilinear", align_corners=align)
+    else:
+        yr = F.interpolate(xr, size=out, mode="bilinear", align_corners=align)
+    dy = rnd(*yr.shape, seed=51)
+    yr.backward(dy)
+    xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV).requires_grad_()
+    yg = mf.interpolate_bilinear(xg, size=None if sf else out, scale_factor=sf, align_corners=align)
+    yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+    close(yg.permute(0, 3, 1, 2), yr)
+    close(xg.grad.permute(0, 3, 1, 2), xr.grad, rtol=1e-5)
+
+
+@pytest.mark.parametrize("is_bn,groups,act", [(True, 0, 2), (True, 0, 0), (False, 256, 2), (False, 4, 0)])
+def test_channel_norm(mf, is_bn, groups, act):
+    from mdemi import _lib as L
+    n, c, h, w = 4, 512 if not is_bn else 48, 3, 5
+    x = rnd(n, c, h, w, seed=60, scale=3) + 1
+    g, b = rnd(c, seed=61), rnd(c, seed=62)
+    dy = rnd(n, c, h, w, seed=63)
+    xr, gr, br = [t.clone().requires_grad_() for t in (x, g, b)]
+    if is_bn:
+        yr = F.batch_norm(xr, None, None, gr, br, training=True, eps=1e-5)
+    else:
+        yr = F.group_norm(xr, groups, gr, br, eps=1e-5)
+    if act == L.ACT_RELU:
+        yr = F.relu(yr)
+    yr.backward(dy)
+    xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV).requires_grad_()
+    gg, bg = g.float().to(DEV).requires_grad_(), b.float().to(DEV).requires_grad_()
+    if is_bn:
+        yg, _, _ = mf.batch_norm_nhwc(xg, gg, bg, 1e-5, act)
+    else:
+        yg = mf.group_norm_nhwc(xg, gg, bg, groups, 1e-5, act)
+    yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+    close(yg.permute(0, 3, 1, 2), yr, rtol=1e-5)
+    close(xg.grad.permute(0, 3, 1, 2), xr.grad, rtol=1e-4)
+    close(gg.grad, gr.grad, rtol=1e-4)
+    close(bg.grad, br.grad, rtol=1e-4)
+
+
+def test_pixel_shuffle_avgpool_patch(mf):
+    n, c, h, w = 2, 16, 5, 7
+    x = rnd(n, c, h, w, seed=70)
+    xr = x.clone().requires_grad_()
+    yr = F.pixel_shuffle(xr, 2)
+    dy = rnd(*yr.shape, seed=71)
+    yr.backward(dy)
+    xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV).requires_grad_()
+    yg = mf.pixel_shuffle_nhwc(xg, 2)
+    yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+    # a pure permutation: bit-exact against the fp32-rounded reference
+    close(yg.permute(0, 3, 1, 2), yr.float(), rtol=0, atol=0)
+    close(xg.grad.permute(0, 3, 1, 2), xr.grad.float(), rtol=0, atol=0)
+    for s in (1, 2, 3, 6):
+        x = rnd(n, 12, 11, 19, seed=72 + s)
+        xr = x.clone().requires_grad_()
+        yr = F.adaptive_avg_pool2d(xr, s)
+        dy = rnd(*yr.shape, seed=80 + s)
+        yr.backward(dy)
+        xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV).requires_grad_()
+        yg = mf.adaptive_avg_pool_nhwc(xg, s)
+        yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+        close(yg.permute(0, 3, 1, 2), yr, rtol=1e-5)
+        close(xg.grad.permute(0, 3, 1, 2), xr.grad, rtol=1e-5)
+    img = rnd(2, 3, 22, 30, seed=90)
+    w, b = rnd(24, 3, 4, 4, seed=91), rnd(24, seed=92)
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    yr = F.conv2d(F.pad(img, (0, 2, 0, 2)), wr, br, stride=4)
+    dy = rnd(*yr.shape, seed=93)
+    yr.backward(dy)
+    wg, bg = w.float().to(DEV).requires_grad_(), b.float().to(DEV).requires_grad_()
+    yg = mf.patch_embed(img.float().to(DEV), wg, bg)
+    yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+    close(yg.permute(0, 3, 1, 2), yr, rtol=1e-5)
+    close(wg.grad, wr.grad, rtol=1e-4)
+    close(bg.grad, br.grad, rtol=1e-4)
+    x = rnd(2, 6, 4, 5, seed=94).float().to(DEV)
+    close(mf.nhwc_to_nchw(mf.nchw_to_nhwc(x)), x.cpu(), rtol=0, atol=0)
+    close(mf.nchw_to_nhwc(x), x.cpu().permute(0, 2, 3, 1), rtol=0, atol=0)
