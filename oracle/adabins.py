@@ -1,0 +1,100 @@
+"""CPU restatement of model/Adabins (everything after the EfficientNet-B5
+encoder).  TEST INFRASTRUCTURE ONLY — see oracle/__init__.py.
+Pinned by tests/golden/{adabins_head,mvit}.npz.  The encoder itself is a
+torch.hub download in the reference (unet_adaptive_bins.py:129): parity unpinned.
+"""
+import torch
+import torch.nn.functional as F
+
+
+def bn_train(P, pre, x, eps=1e-5):
+    return F.batch_norm(x, None, None, P[pre + "weight"], P[pre + "bias"], training=True, eps=eps)
+
+
+def upsample_bn(P, pre, x, concat_with):  # unet_adaptive_bins.py:8-24
+    up_x = F.interpolate(x, size=[concat_with.size(2), concat_with.size(3)], mode="bilinear", align_corners=True)
+    f = torch.cat([up_x, concat_with], dim=1)
+    f = F.leaky_relu(bn_train(P, pre + "_net.1.", F.conv2d(f, P[pre + "_net.0.weight"], P[pre + "_net.0.bias"],
+                                                            padding=1)))
+    return F.leaky_relu(bn_train(P, pre + "_net.4.", F.conv2d(f, P[pre + "_net.3.weight"], P[pre + "_net.3.bias"],
+                                                               padding=1)))
+
+
+def decoder_bn(P, pre, features):  # unet_adaptive_bins.py:27-57
+    b0, b1, b2, b3, b4 = features[4], features[5], features[6], features[8], features[11]
+    x = F.conv2d(b4, P[pre + "conv2.weight"], P[pre + "conv2.bias"], padding=1)
+    x = upsample_bn(P, pre + "up1.", x, b3)
+    x = upsample_bn(P, pre + "up2.", x, b2)
+    x = upsample_bn(P, pre + "up3.", x, b1)
+    x = upsample_bn(P, pre + "up4.", x, b0)
+    return F.conv2d(x, P[pre + "conv3.weight"], P[pre + "conv3.bias"], padding=1)
+
+
+def transformer_encoder_layer(P, pre, src, heads):
+    """nn.TransformerEncoderLayer(E, heads, 1024) defaults: post-norm, ReLU, (S,N,E) layout."""
+    S, N, E = src.shape
+    hd = E // heads
+    qkv = F.linear(src, P[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"])
+    q, k, v = qkv.chunk(3, dim=-1)
+
+    def heads_first(t):
+        return t.contiguous().view(S, N * heads, hd).transpose(0, 1)
+
+    q, k, v = heads_first(q), heads_first(k), heads_first(v)
+    attn = torch.softmax((q @ k.transpose(-2, -1)) / (hd ** 0.5), dim=-1)
+    o = (attn @ v).transpose(0, 1).contiguous().view(S, N, E)
+    o = F.linear(o, P[pre + "self_attn.out_proj.weight"], P[pre + "self_attn.out_proj.bias"])
+    x = F.layer_norm(src + o, (E,), P[pre + "norm1.weight"], P[pre + "norm1.bias"], 1e-5)
+    ff = F.linear(F.relu(F.linear(x, P[pre + "linear1.weight"], P[pre + "linear1.bias"])),
+                  P[pre + "linear2.weight"], P[pre + "linear2.bias"])
+    return F.layer_norm(x + ff, (E,), P[pre + "norm2.weight"], P[pre + "norm2.bias"], 1e-5)
+
+
+def patch_transformer(P, pre, x, patch_size=16, heads=4, layers=4):  # layers.py:22-31
+    emb = F.conv2d(x, P[pre + "embedding_encoder.weight"], P[pre + "embedding_encoder.bias"],
+                   stride=patch_size).flatten(2)
+    emb = emb + P[pre + "positional_encodings"][:emb.shape[2], :].T.unsqueeze(0)
+    t = emb.permute(2, 0, 1)
+    for i in range(layers):
+        t = transformer_encoder_layer(P, f"{pre}transformer_encoder.layers.{i}.", t, heads)
+    return t
+
+
+def pixel_wise_dot(x, K):  # layers.py:38-43
+    n, c, h, w = x.size()
+    y = torch.matmul(x.view(n, c, h * w).permute(0, 2, 1), K.permute(0, 2, 1))
+    return y.permute(0, 2, 1).view(n, K.shape[1], h, w)
+
+
+def mvit(P, pre, x, n_query_channels=128, patch_size=16, norm="linear"):  # miniViT.py:25-48
+    tgt = patch_transformer(P, pre + "patch_transformer.", x.clone(), patch_size)
+    x = F.conv2d(x, P[pre + "embedding_conv.weight"], P[pre + "embedding_conv.bias"], padding=1)
+    head, queries = tgt[0, ...], tgt[1:n_query_channels + 1, ...]
+    range_maps = pixel_wise_dot(x, queries.permute(1, 0, 2))
+    y = F.leaky_relu(F.linear(head, P[pre + "regressor.0.weight"], P[pre + "regressor.0.bias"]))
+    y = F.leaky_relu(F.linear(y, P[pre + "regressor.2.weight"], P[pre + "regressor.2.bias"]))
+    y = F.linear(y, P[pre + "regressor.4.weight"], P[pre + "regressor.4.bias"])
+    if norm == "linear":
+        y = torch.relu(y) + 0.1
+    elif norm == "softmax":
+        return torch.softmax(y, dim=1), range_maps
+    else:
+        y = torch.sigmoid(y)
+    return y / y.sum(dim=1, keepdim=True), range_maps
+
+
+def bins_to_pred(probs, bin_widths_normed, min_val, max_val):  # unet_adaptive_bins.py:99-107
+    bin_widths = (max_val - min_val) * bin_widths_normed
+    bin_widths = F.pad(bin_widths, (1, 0), mode="constant", value=min_val)
+    bin_edges = torch.cumsum(bin_widths, dim=1)
+    centers = 0.5 * (bin_edges[:, :-1] + bin_edges[:, 1:])
+    n, dout = centers.size()
+    pred = torch.sum(probs * centers.view(n, dout, 1, 1), dim=1, keepdim=True)
+    return pred, bin_edges
+
+
+def adabins_head(P, features, min_val=1e-3, max_val=10.0):  # unet_adaptive_bins.py:93-109 after the encoder
+    unet_out = decoder_bn(P, "decoder.", features)
+    widths, range_maps = mvit(P, "adaptive_bins_layer.", unet_out)
+    probs = torch.softmax(F.conv2d(range_maps, P["conv_out.0.weight"], P["conv_out.0.bias"]), dim=1)
+    return bins_to_pred(probs, widths, min_val, max_val)

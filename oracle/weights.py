@@ -1,0 +1,32 @@
+"""Deterministic weights and inputs shared by the golden generator and the tests.
+
+closed_form_fill: every floating state_dict entry, in state_dict order, gets
+    w[i] = scale * sin(0.7 * i + seed)            (i = running element index)
+    1-D ``*weight`` entries (norm scales) and running_var: 1 + scale*sin(...)
+so the GPU box can rebuild the exact weights from the formula — and a model
+whose state_dict keys/shapes/order differ from the reference's gets different
+weights (the fill doubles as a structural check).
+"""
+import numpy as np
+import torch
+
+
+def closed_form_fill(state_dict, seed=0.0, scale=0.05):
+    off = 0
+    with torch.no_grad():
+        for name, t in state_dict.items():
+            if not torch.is_floating_point(t):
+                continue
+            n = t.numel()
+            i = torch.arange(off, off + n, dtype=torch.float64)
+            vals = scale * torch.sin(0.7 * i + seed)
+            if (t.dim() == 1 and name.endswith("weight")) or name.endswith("running_var"):
+                vals = 1.0 + vals
+            t.copy_(vals.view_as(t).to(t.dtype))
+            off += n
+    return off
+
+
+def rng_array(shape, seed=0):
+    g = np.random.Generator(np.random.PCG64(seed))
+    return g.standard_normal(size=shape).astype(np.float32)
