@@ -109,6 +109,16 @@ size_t mdemi_colsum_workspace_size(int64_t rows, int64_t cols);
 int mdemi_colsum_f32(const float* x, int64_t rows, int64_t cols, int64_t ld,
                      float* out, int accumulate, void* workspace, void* stream);
 
+/* KxK 'same' conv to ONE output channel over NHWC (DispHead.conv1,
+ * NewCRFDepth.py:155): memory-bound sweep instead of an N=1 GEMM.  w is in the
+ * reference layout [1][C][K][K]; dx/dw/db may be NULL to skip that gradient. */
+int mdemi_headconv_fwd(const float* x, const float* w, const float* b, float* y, int32_t N,
+                       int32_t H, int32_t W, int32_t C, int32_t K, int32_t pad, void* stream);
+size_t mdemi_headconv_wgrad_workspace_size(int32_t N, int32_t H, int32_t W, int32_t C, int32_t K);
+int mdemi_headconv_bwd(const float* dy, const float* x, const float* w, float* dx, float* dw,
+                       float* db, int32_t N, int32_t H, int32_t W, int32_t C, int32_t K, int32_t pad,
+                       void* workspace, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Adaptive-bin depth head (unet_adaptive_bins.py:97-107,                   */
 /* depthformer_v8.py:62-73, decoder_v8.py:158-159):                          */
@@ -219,6 +229,16 @@ int mdemi_pixel_shuffle_nhwc(const float* x, float* y, int32_t N, int32_t H, int
 int mdemi_patchify_nchw(const float* img, float* cols, int32_t N, int32_t C, int32_t H,
                         int32_t W, int32_t p, int32_t inverse, void* stream);
 
+/* PatchMerging 2x2 gather (swin_transformer.py:272-284): [N,H,W,C] ->
+ * [N,ceil(H/2),ceil(W/2),4C] in the reference's (0,0),(1,0),(0,1),(1,1) order,
+ * zero-padded for odd sizes.  inverse=1 writes the adjoint into x (from y). */
+int mdemi_space_to_depth2(const float* x, float* y, int32_t N, int32_t H, int32_t W, int32_t C,
+                          int32_t inverse, void* stream);
+/* strided 2-D copy (channel-slice concat/split, torch.cat in uper_crf_head.py:355,
+ * unet_adaptive_bins.py:23, layer_utils.py:116) */
+int mdemi_copy2d(const float* src, int64_t src_ld, float* dst, int64_t dst_ld, int64_t rows,
+                 int64_t cols, int32_t accumulate, void* stream);
+
 /* adaptive average pooling, NHWC (nn.AdaptiveAvgPool2d, uper_crf_head.py:38) */
 int mdemi_adaptive_avgpool_fwd(const float* x, float* y, int32_t N, int32_t H, int32_t W,
                                int32_t C, int32_t OH, int32_t OW, void* stream);
@@ -243,6 +263,11 @@ int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y, const floa
                      float* dgamma, float* dbeta, int32_t N, int64_t HW, int32_t C,
                      int32_t groups, int32_t is_bn, int32_t act, void* workspace, void* stream);
 
+/* inference-mode normalisation with caller-supplied statistics (BN eval) */
+int mdemi_chnorm_apply(const float* x, const float* gamma, const float* beta, const float* mean,
+                       const float* rstd, float* y, int32_t N, int64_t HW, int32_t C, int32_t groups,
+                       int32_t is_bn, int32_t act, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Elementwise helpers                                                       */
 /* ------------------------------------------------------------------------ */
@@ -253,6 +278,10 @@ int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y, const floa
 #define MDEMI_EW_ACT_BWD 4    /* y = b * act'(a), act given in `s` as an MDEMI_ACT_* code */
 int mdemi_elementwise(int32_t op, const float* a, const float* b, float* y, int64_t n,
                       float s, float t, void* stream);
+/* stochastic depth residual (timm DropPath, swin_transformer.py:243-244):
+ * y = (a ? a : 0) + b * scale[i / per_group] */
+int mdemi_rowscale_add(const float* a, const float* b, const float* scale, float* y,
+                       int64_t per_group, int64_t n, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Optimizer (restated; reference run.py is missing): multi-tensor AdamW    */

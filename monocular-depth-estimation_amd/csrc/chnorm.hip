@@ -276,3 +276,16 @@ extern "C" int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y,
   }
   return check_launch("chnorm_bwd");
 }
+
+// Inference-mode normalisation with given statistics (BatchNorm eval path:
+// running stats folded into mean/rstd by the caller).
+extern "C" int mdemi_chnorm_apply(const float* x, const float* gamma, const float* beta, const float* mean,
+                                  const float* rstd, float* y, int32_t N, int64_t HW, int32_t C, int32_t groups,
+                                  int32_t is_bn, int32_t act, void* stream) {
+  MDEMI_REQUIRE(x && gamma && beta && mean && rstd && y && N > 0 && HW > 0 && C > 0, "chnorm_apply: bad args");
+  const int G = is_bn ? C : groups;
+  MDEMI_REQUIRE(G > 0 && C % G == 0, "chnorm_apply: bad groups");
+  hipLaunchKernelGGL(chnorm_apply, dim3(grid_for((int64_t)N * HW * C)), dim3(CN_THREADS), 0, (hipStream_t)stream, x,
+                     gamma, beta, mean, rstd, y, N, HW, C, G, is_bn, act);
+  return check_launch("chnorm_apply");
+}

@@ -212,3 +212,27 @@ extern "C" int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t nte
                      ci, g, sumsq, max_norm, 0.f, 0.f, step);
   return check_launch("adamw_step");
 }
+
+// Stochastic depth (timm DropPath, swin_transformer.py:181,243-244):
+// y = (a ? a : 0) + b * scale[row / rows_per_group]  (scale = keep/(1-p) per sample)
+namespace mdemi {
+__global__ __launch_bounds__(256) void rowscale_add_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                           const float* __restrict__ scale, float* __restrict__ y,
+                                                           int64_t per_group, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float s = scale[i / per_group];
+    y[i] = (a ? a[i] : 0.f) + b[i] * s;
+  }
+}
+}  // namespace mdemi
+
+extern "C" int mdemi_rowscale_add(const float* a, const float* b, const float* scale, float* y, int64_t per_group,
+                                  int64_t n, void* stream) {
+  MDEMI_REQUIRE(b && scale && y && per_group > 0 && n >= 0, "rowscale_add: bad args");
+  if (n == 0) return MDEMI_OK;
+  int64_t nb = cdiv(n, 256);
+  nb = nb < 8192 ? nb : 8192;
+  hipLaunchKernelGGL(rowscale_add_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, a, b, scale, y,
+                     per_group, n);
+  return check_launch("rowscale_add");
+}

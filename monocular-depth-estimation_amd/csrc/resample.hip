@@ -329,3 +329,78 @@ extern "C" int mdemi_nhwc_to_nchw(const float* x, float* y, int32_t N, int32_t C
   MDEMI_REQUIRE(x && y && N > 0 && C > 0 && HW > 0, "nhwc_to_nchw: bad args");
   return launch_transpose(x, y, N, HW, C, stream);
 }
+
+// ---------------------------------------------------------------------------
+// PatchMerging gather (swin_transformer.py:272-284): y[b,i,j] = cat(x[2i,2j],
+// x[2i+1,2j], x[2i,2j+1], x[2i+1,2j+1]) with zero padding for odd H/W; the
+// inverse is its adjoint (the backward), dropping the pad positions.
+// ---------------------------------------------------------------------------
+namespace mdemi {
+__global__ void space_to_depth2_kernel(const float* __restrict__ x, float* __restrict__ y, int N, int H, int W,
+                                       int C, int inverse) {
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;
+  const int C4 = C / 4;
+  const int64_t total = (int64_t)N * OH * OW * 4 * C4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(e % C4);
+    int64_t t = e / C4;
+    const int q = (int)(t % 4); t /= 4;
+    const int j = (int)(t % OW); t /= OW;
+    const int i = (int)(t % OH);
+    const int n = (int)(t / OH);
+    const int yy = 2 * i + (q & 1), xx = 2 * j + (q >> 1);
+    float4* dst = reinterpret_cast<float4*>(y) + e;
+    const bool in = yy < H && xx < W;
+    const int64_t src = ((((int64_t)n * H + yy) * W + xx) * C) / 4 + c4;
+    if (!inverse) *dst = in ? reinterpret_cast<const float4*>(x)[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+    else if (in) reinterpret_cast<float4*>(const_cast<float*>(x))[src] = *dst;
+  }
+}
+}  // namespace mdemi
+
+extern "C" int mdemi_space_to_depth2(const float* x, float* y, int32_t N, int32_t H, int32_t W, int32_t C,
+                                     int32_t inverse, void* stream) {
+  MDEMI_REQUIRE(x && y && N > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0, "space_to_depth2: bad args");
+  const int64_t total = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * C;
+  // inverse: x is the destination (dx), y the source (dy)
+  hipLaunchKernelGGL(space_to_depth2_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, y, N, H, W,
+                     C, inverse);
+  return check_launch("space_to_depth2");
+}
+
+// 2-D strided copy (channel-slice concat / split of NHWC maps)
+namespace mdemi {
+template <int VEC>
+__global__ void copy2d_kernel(const float* __restrict__ src, int64_t sld, float* __restrict__ dst, int64_t dld,
+                              int64_t rows, int64_t cols, int accumulate) {
+  const int64_t cv = cols / VEC;
+  const int64_t total = rows * cv;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / cv, c = (e % cv) * VEC;
+    if (VEC == 4) {
+      float4 v = *reinterpret_cast<const float4*>(src + r * sld + c);
+      float4* d = reinterpret_cast<float4*>(dst + r * dld + c);
+      if (accumulate) { const float4 o = *d; v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w; }
+      *d = v;
+    } else {
+      const float v = src[r * sld + c];
+      dst[r * dld + c] = accumulate ? dst[r * dld + c] + v : v;
+    }
+  }
+}
+}  // namespace mdemi
+
+extern "C" int mdemi_copy2d(const float* src, int64_t src_ld, float* dst, int64_t dst_ld, int64_t rows, int64_t cols,
+                            int32_t accumulate, void* stream) {
+  MDEMI_REQUIRE(src && dst && rows > 0 && cols > 0 && src_ld >= cols && dst_ld >= cols, "copy2d: bad args");
+  const bool v4 = cols % 4 == 0 && src_ld % 4 == 0 && dst_ld % 4 == 0 && ((uintptr_t)src & 15) == 0 &&
+                  ((uintptr_t)dst & 15) == 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (v4)
+    hipLaunchKernelGGL(copy2d_kernel<4>, dim3(grid_for(rows * cols / 4)), dim3(256), 0, st, src, src_ld, dst, dst_ld,
+                       rows, cols, accumulate);
+  else
+    hipLaunchKernelGGL(copy2d_kernel<1>, dim3(grid_for(rows * cols)), dim3(256), 0, st, src, src_ld, dst, dst_ld, rows,
+                       cols, accumulate);
+  return check_launch("copy2d");
+}

@@ -95,6 +95,9 @@ _SIGS = {
     "mdemi_gemm_f32": (ctypes.c_int, [ctypes.POINTER(GemmDesc), vp]),
     "mdemi_colsum_workspace_size": (sz, [i64, i64]),
     "mdemi_colsum_f32": (ctypes.c_int, [vp, i64, i64, i64, vp, ctypes.c_int, vp, vp]),
+    "mdemi_headconv_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "mdemi_headconv_wgrad_workspace_size": (sz, [i32, i32, i32, i32, i32]),
+    "mdemi_headconv_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]),
     "mdemi_binhead_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i32, i64, i32, vp]),
     "mdemi_binhead_bwd_workspace_size": (sz, [i32, i32, i64]),
     "mdemi_binhead_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i64, i32, vp, vp]),
@@ -120,6 +123,10 @@ _SIGS = {
     "mdemi_chnorm_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32,
                                         vp, vp]),
     "mdemi_elementwise": (ctypes.c_int, [i32, vp, vp, vp, i64, f32, f32, vp]),
+    "mdemi_rowscale_add": (ctypes.c_int, [vp, vp, vp, vp, i64, i64, vp]),
+    "mdemi_space_to_depth2": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
+    "mdemi_copy2d": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, i32, vp]),
+    "mdemi_chnorm_apply": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp]),
     "mdemi_multi_tensor_chunk": (ctypes.c_int, []),
     "mdemi_grad_norm_workspace_size": (sz, [i32]),
     "mdemi_grad_sumsq": (ctypes.c_int, [vp, i32, i64, vp, vp, vp]),

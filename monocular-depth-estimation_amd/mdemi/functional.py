@@ -177,7 +177,7 @@ class _Conv2dFn(torch.autograd.Function):
             if c % 4:
                 raise ValueError("conv2d: implicit-GEMM path needs C % 4 == 0")
             gemm(x, wf, out, M, cout, K, lda=0, ldb=K, ldc=cout, a_layout=L.L_CONV, b_layout=L.L_KCONTIG,
-                 bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act, split_k=1,
+                 bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act,
                  conv=_geom(n, h, w, c, oh, ow, kh, kw, stride, pad, pad_mode))
         ctx.save_for_backward(x, weight, out if act != L.ACT_NONE else None)
         ctx.cfg = (stride, pad, pad_mode, act, bias is not None, pointwise)
@@ -227,7 +227,42 @@ class _Conv2dFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+class _HeadConvFn(torch.autograd.Function):
+    """KxK 'same' conv with a single output channel (DispHead.conv1)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        _require_cuda(x, weight, bias)
+        x, weight = _c(x), _c(weight)
+        n, h, w, c = x.shape
+        k = weight.shape[-1]
+        y = torch.empty(n, h, w, 1, device=x.device, dtype=torch.float32)
+        L.call("mdemi_headconv_fwd", x.data_ptr(), weight.data_ptr(), L.ptr(bias), y.data_ptr(), n, h, w, c, k,
+               k // 2, L.stream())
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy = _c(dy)
+        n, h, w, c = x.shape
+        k = weight.shape[-1]
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(weight) if ctx.needs_input_grad[1] else None
+        db = torch.empty(1, device=x.device, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        lib = L.load()
+        ws = L.workspace(lib.mdemi_headconv_wgrad_workspace_size(n, h, w, c, k), x.device)
+        L.check(lib.mdemi_headconv_bwd(dy.data_ptr(), x.data_ptr(), weight.data_ptr(), L.ptr(dx), L.ptr(dw), L.ptr(db),
+                                       n, h, w, c, k, k // 2, ws.data_ptr(), L.stream()), "headconv_bwd")
+        return dx, dw, db
+
+
 def conv2d_nhwc(x, weight, bias=None, stride=1, pad=0, pad_mode=L.PAD_ZERO, act=L.ACT_NONE):
+    if weight.shape[0] == 1 and stride == 1 and pad_mode == L.PAD_ZERO and act == L.ACT_NONE and \
+            2 * pad == weight.shape[-1] - 1 and x.shape[-1] % 4 == 0:
+        return _HeadConvFn.apply(x, weight, bias)
     return _Conv2dFn.apply(x, weight, bias, stride, pad, pad_mode, act)
 
 
@@ -711,3 +746,119 @@ class _AddFn(torch.autograd.Function):
 
 def add(a, b):
     return _AddFn.apply(a, b)
+
+
+# --------------------------------------------------------------------------
+# PatchMerging gather, channel concat, stochastic depth
+# --------------------------------------------------------------------------
+
+
+class _SpaceToDepth2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        _require_cuda(x)
+        x = _c(x)
+        n, h, w, c = x.shape
+        y = torch.empty(n, (h + 1) // 2, (w + 1) // 2, 4 * c, device=x.device, dtype=torch.float32)
+        L.call("mdemi_space_to_depth2", x.data_ptr(), y.data_ptr(), n, h, w, c, 0, L.stream())
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c = ctx.shape
+        dy = _c(dy)
+        dx = torch.empty(n, h, w, c, device=dy.device, dtype=torch.float32)
+        L.call("mdemi_space_to_depth2", dx.data_ptr(), dy.data_ptr(), n, h, w, c, 1, L.stream())
+        return dx
+
+
+def space_to_depth2(x_nhwc):
+    """PatchMerging's x0..x3 gather + cat (swin_transformer.py:272-284), NHWC."""
+    return _SpaceToDepth2Fn.apply(x_nhwc)
+
+
+def _copy2d(src2, dst2, accumulate=False):
+    rows, cols = src2.shape
+    L.call("mdemi_copy2d", src2.data_ptr(), src2.stride(0), dst2.data_ptr(), dst2.stride(0), rows, cols,
+           int(accumulate), L.stream())
+
+
+class _ConcatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        _require_cuda(*xs)
+        xs = [_c(x) for x in xs]
+        lead = xs[0].shape[:-1]
+        widths = [x.shape[-1] for x in xs]
+        out = torch.empty(*lead, sum(widths), device=xs[0].device, dtype=torch.float32)
+        o2 = out.view(-1, out.shape[-1])
+        off = 0
+        for x, wd in zip(xs, widths):
+            _copy2d(x.view(-1, wd), o2[:, off:off + wd])
+            off += wd
+        ctx.widths = widths
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = _c(dy)
+        d2 = dy.view(-1, dy.shape[-1])
+        grads = []
+        off = 0
+        for wd in ctx.widths:
+            g = torch.empty(*dy.shape[:-1], wd, device=dy.device, dtype=torch.float32)
+            _copy2d(d2[:, off:off + wd], g.view(-1, wd))
+            grads.append(g)
+            off += wd
+        return tuple(grads)
+
+
+def concat_channels(xs):
+    """torch.cat(dim=1) of NCHW maps == channel concat of NHWC maps."""
+    return _ConcatFn.apply(*xs)
+
+
+class _DropPathAddFn(torch.autograd.Function):
+    """y = res + branch * scale[sample]  (timm DropPath with scale = keep / (1 - p))."""
+
+    @staticmethod
+    def forward(ctx, res, branch, scale):
+        res, branch = _c(res), _c(branch)
+        y = torch.empty_like(branch)
+        per = branch.numel() // scale.numel()
+        L.call("mdemi_rowscale_add", res.data_ptr(), branch.data_ptr(), scale.data_ptr(), y.data_ptr(), per,
+               branch.numel(), L.stream())
+        ctx.save_for_backward(scale)
+        ctx.per = per
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (scale,) = ctx.saved_tensors
+        dy = _c(dy)
+        db = torch.empty_like(dy)
+        L.call("mdemi_rowscale_add", None, dy.data_ptr(), scale.data_ptr(), db.data_ptr(), ctx.per, dy.numel(),
+               L.stream())
+        return dy, db, None
+
+
+def drop_path_add(res, branch, drop_prob, training):
+    if drop_prob == 0.0 or not training:
+        return add(res, branch)
+    keep = 1.0 - drop_prob
+    scale = torch.empty(branch.shape[0], device=branch.device, dtype=torch.float32).bernoulli_(keep).div_(keep)
+    return _DropPathAddFn.apply(res, branch, scale)
+
+
+def batch_norm_eval_nhwc(x, weight, bias, running_mean, running_var, eps=1e-5, act=L.ACT_NONE):
+    """Inference BatchNorm2d (running statistics); no autograd."""
+    _require_cuda(x)
+    x = _c(x)
+    n, c = x.shape[0], x.shape[-1]
+    hw = x[0].numel() // c
+    rstd = torch.rsqrt(running_var + eps)
+    y = torch.empty_like(x)
+    L.call("mdemi_chnorm_apply", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), running_mean.data_ptr(),
+           rstd.data_ptr(), y.data_ptr(), n, hw, c, c, 1, act, L.stream())
+    return y

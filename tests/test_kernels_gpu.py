@@ -340,3 +340,66 @@ def test_pixel_shuffle_avgpool_patch(mf):
     x = rnd(2, 6, 4, 5, seed=94).float().to(DEV)
     close(mf.nhwc_to_nchw(mf.nchw_to_nhwc(x)), x.cpu(), rtol=0, atol=0)
     close(mf.nchw_to_nhwc(x), x.cpu().permute(0, 2, 3, 1), rtol=0, atol=0)
+
+
+def test_fused_adamw_with_clip_matches_torch(mf):
+    from mdemi.train import FusedAdamW
+    torch.manual_seed(0)
+    shapes = [(300, 7), (5,), (70000,), (3, 4, 5)]
+    ps = [torch.randn(*s, device=DEV) for s in shapes]
+    pr = [p.clone().requires_grad_() for p in ps]
+    pg = [p.clone().requires_grad_() for p in ps]
+    ref = torch.optim.AdamW(pr, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1)
+    opt = FusedAdamW(pg, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, max_grad_norm=0.5)
+    for it in range(3):
+        grads = [torch.randn(*s, device=DEV) * (it + 1) for s in shapes]
+        for p, g in zip(pr, grads):
+            p.grad = g.clone()
+        for p, g in zip(pg, grads):
+            p.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_(pr, 0.5)
+        ref.step()
+        opt.step()
+    for a, b in zip(pg, pr):
+        close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_headconv(mf):
+    n, c, h, w = 2, 128, 9, 11
+    x, wt, b = rnd(n, c, h, w, seed=100), rnd(1, c, 3, 3, seed=101, scale=0.1), rnd(1, seed=102)
+    xr, wr, br = [t.clone().requires_grad_() for t in (x, wt, b)]
+    yr = F.conv2d(xr, wr, br, padding=1)
+    dy = rnd(*yr.shape, seed=103)
+    yr.backward(dy)
+    xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV).requires_grad_()
+    wg, bg = wt.float().to(DEV).requires_grad_(), b.float().to(DEV).requires_grad_()
+    yg = mf.conv2d_nhwc(xg, wg, bg, stride=1, pad=1)
+    yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+    close(yg.permute(0, 3, 1, 2), yr, rtol=1e-5)
+    close(xg.grad.permute(0, 3, 1, 2), xr.grad, rtol=1e-5)
+    close(wg.grad, wr.grad, rtol=1e-4)
+    close(bg.grad, br.grad, rtol=1e-4)
+
+
+def test_space_to_depth_concat_droppath(mf):
+    n, h, w, c = 2, 9, 13, 8
+    x = rnd(n, h, w, c, seed=110)
+    xr = x.clone().requires_grad_()
+    xp = F.pad(xr, (0, 0, 0, w % 2, 0, h % 2))
+    yr = torch.cat([xp[:, 0::2, 0::2], xp[:, 1::2, 0::2], xp[:, 0::2, 1::2], xp[:, 1::2, 1::2]], -1)
+    dy = rnd(*yr.shape, seed=111)
+    yr.backward(dy)
+    xg = x.float().to(DEV).requires_grad_()
+    yg = mf.space_to_depth2(xg)
+    yg.backward(dy.float().to(DEV))
+    close(yg, yr.float(), rtol=0, atol=0)
+    close(xg.grad, xr.grad.float(), rtol=0, atol=0)
+    a, b = rnd(4, 5, 8, seed=112).float().to(DEV), rnd(4, 5, 12, seed=113).float().to(DEV)
+    cat = mf.concat_channels([a, b])
+    close(cat, torch.cat([a, b], -1).cpu(), rtol=0, atol=0)
+    res, br = rnd(4, 30, seed=114).float().to(DEV), rnd(4, 30, seed=115).float().to(DEV).requires_grad_()
+    torch.manual_seed(0)
+    y = mf.drop_path_add(res, br, 0.5, True)
+    kept = (y - res).abs().sum(1) > 0
+    exp = res + br.detach() * 2.0 * kept.float().unsqueeze(1)
+    close(y, exp.cpu(), rtol=1e-6, atol=1e-6)

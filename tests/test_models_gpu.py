@@ -1,0 +1,148 @@
+"""Model-level parity on the GPU: the mdemi modules (libmdemi kernels, NHWC
+inside) against golden vectors produced by the reference itself, with the
+reference's weights rebuilt from the closed-form fill and identical inputs.
+Forward outputs and every parameter/input gradient are compared
+(fp32 kernels vs the fp32 reference: tolerances stated per check)."""
+import pytest
+import torch
+
+from golden_util import Golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RT_OUT, RT_GRAD = 1e-4, 1e-3
+
+
+def nchw_to_nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nhwc_to_nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def load_golden_weights(model, g):
+    from oracle.weights import closed_form_fill
+    sd = model.state_dict()
+    cpu = {k: v.detach().cpu().clone() for k, v in sd.items()}
+    closed_form_fill(cpu, seed=g.fill[0], scale=g.fill[1])
+    with torch.no_grad():
+        for k, v in sd.items():
+            if torch.is_floating_point(v):
+                v.copy_(cpu[k])
+    return model
+
+
+def run_case(g, model, fwd, out_names, out_layouts, in_layouts, no_input_grad=()):
+    """in_layouts/out_layouts: name -> 'nchw' (converted to/from NHWC) or 'same'.
+    no_input_grad: inputs the product never differentiates (the input image)."""
+    model = load_golden_weights(model.to(DEV), g)
+    model.train()
+    model.zero_grad(set_to_none=True)
+    ins = {}
+    for n in g.input_names():
+        t = g.input(n, torch.float32)
+        if in_layouts.get(n) == "nchw":
+            t = nchw_to_nhwc(t)
+        ins[n] = t.to(DEV).requires_grad_(True)
+    outs = fwd(model, ins)
+    if not isinstance(outs, (tuple, list)):
+        outs = (outs,)
+    loss = 0
+    for name, o in zip(out_names, outs):
+        oc = nhwc_to_nchw(o) if out_layouts.get(name) == "nchw" else o
+        g.check(f"out/{name}", oc.float().cpu(), RT_OUT, 1e-5)
+        dy = g.dy(name, oc.shape, torch.float32).to(DEV)
+        if out_layouts.get(name) == "nchw":
+            dy = nchw_to_nhwc(dy)
+        loss = loss + (o * dy).sum()
+    loss.backward()
+    for n, t in ins.items():
+        if n in no_input_grad:
+            assert t.grad is None
+            continue
+        if g.has(f"grad/{n}"):
+            gr = nhwc_to_nchw(t.grad) if in_layouts.get(n) == "nchw" else t.grad
+            g.check(f"grad/{n}", gr.cpu(), RT_GRAD, 1e-5)
+    n_checked = 0
+    for k, p in model.named_parameters():
+        if g.has(f"grad/{k}"):
+            g.check(f"grad/{k}", p.grad.cpu(), RT_GRAD, 1e-5)
+            n_checked += 1
+        elif f"gsum/{k}" in g.d:
+            s = g.d[f"gsum/{k}"]
+            gv = p.grad.double().cpu()
+            tol = 2e-3
+            assert abs(gv.sum().item() - s[0]) <= tol * (s[1] * gv.numel()) ** 0.5 + 1e-6, k
+            assert abs((gv * gv).sum().item() - s[1]) <= 2 * tol * s[1] + 1e-12, k
+            n_checked += 1
+    return n_checked
+
+
+@pytest.mark.parametrize("hw", [(10, 12), (9, 13)])
+def test_swin_basic_layer(hw):
+    from mdemi.model.NewCRFs.swin_transformer import BasicLayer, PatchMerging
+    H, W = hw
+    g = Golden(f"swin_basic_layer_{H}x{W}")
+    m = BasicLayer(dim=64, depth=2, num_heads=2, window_size=7, downsample=PatchMerging)
+
+    def fwd(m, i):
+        r = m(i["x"], H, W)
+        return r[0], r[3]
+
+    assert run_case(g, m, fwd, ["x_out", "x_down"], {}, {}) == len(list(m.parameters()))
+
+
+def test_swin_window_attention_unshifted_windows():
+    """WindowAttention on pre-partitioned windows == 7x7 images, shift 0."""
+    from mdemi import functional as mf
+    from mdemi.model.NewCRFs.swin_transformer import WindowAttention
+    g = Golden("swin_window_attention")
+    m = WindowAttention(64, (7, 7), 2)
+
+    def fwd(m, i):
+        x = i["x"].reshape(-1, 64)
+        a = m.attend(x, 6, 7, 7, 0)
+        return mf.linear(a, m.proj.weight, m.proj.bias).view(6, 49, 64)
+
+    run_case(g, m, fwd, ["y"], {}, {})
+
+
+def test_swin_backbone():
+    from mdemi.model.NewCRFs.swin_transformer import SwinTransformer
+    g = Golden("swin_backbone")
+    m = SwinTransformer(embed_dim=64, depths=[2, 2, 2, 2], num_heads=[2, 4, 8, 16], window_size=7, drop_path_rate=0.0)
+    n = run_case(g, m, lambda m, i: m(i["img"]), ["o0", "o1", "o2", "o3"], {f"o{k}": "nchw" for k in range(4)}, {},
+                 no_input_grad=("img",))
+    assert n == len(list(m.parameters()))
+
+
+def test_newcrf_layer():
+    from mdemi.model.NewCRFs.newcrf_layers import NewCRF
+    g = Golden("newcrf_layer")
+    m = NewCRF(input_dim=96, embed_dim=128, window_size=7, v_dim=64, num_heads=4)
+    run_case(g, m, lambda m, i: m(i["x"], i["v"]), ["y"], {"y": "nchw"}, {"x": "nchw", "v": "nchw"})
+
+
+def test_psp_head():
+    from mdemi.model.NewCRFs.uper_crf_head import PSP
+    g = Golden("psp_head")
+    m = PSP(in_channels=[16, 32, 64, 128], in_index=[0, 1, 2, 3], pool_scales=(1, 2, 3, 6), channels=512,
+            dropout_ratio=0.0, num_classes=32, norm_cfg=dict(type="BN", requires_grad=True), align_corners=False)
+    run_case(g, m, lambda m, i: m([i["f0"], i["f1"], i["f2"], i["f3"]]), ["y"], {"y": "nchw"},
+             {f"f{k}": "nchw" for k in range(4)})
+
+
+def test_disp_head():
+    from mdemi.model.NewCRFs.NewCRFDepth import DispHead
+    g = Golden("disp_head")
+    m = DispHead(input_dim=128)
+    run_case(g, m, lambda m, i: m(i["x"], 4), ["y"], {"y": "nchw"}, {"x": "nchw"})
+
+
+def test_newcrfs_tiny07_end_to_end():
+    from mdemi.model.NewCRFs import NewCRFDepth
+    g = Golden("newcrfs_tiny07")
+    m = NewCRFDepth(version="tiny07", max_depth=10.0, drop_path_rate=0.0)
+    n = run_case(g, m, lambda m, i: m(i["img"]), ["depth"], {}, {}, no_input_grad=("img",))
+    assert n == len(list(m.parameters()))
