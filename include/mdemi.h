@@ -102,6 +102,9 @@ typedef struct mdemi_gemm_desc {
 
 size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d);
 int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream);
+/* tuning hook: pipelining variant (0..4, see gemm_f32.hip) and tile raster
+ * (group_m > 0: XCD-aware grouped raster, 0: plain).  Process-global. */
+int mdemi_gemm_set_variant(int32_t variant, int32_t group_m);
 
 /* column / row sums (bias gradients: db[j] = sum_i dY[i][j])
  * replaces the bias-grad reduction autograd runs for every nn.Linear/Conv2d. */

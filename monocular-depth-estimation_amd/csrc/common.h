@@ -86,6 +86,13 @@ __device__ __forceinline__ float act_grad(int act, float x, float y) {
 }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Deterministic column sum of a row-major [rows][cols] matrix (row pitch ld):
+// out[c] (+)= sum_r x[r][c].  Used for bias gradients and for every
+// "per-block partial rows" reduction in the library.  ws: colsum_ws_bytes().
+size_t colsum_ws_bytes(int64_t rows, int64_t cols);
+int colsum_launch(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, int accumulate, void* ws,
+                  hipStream_t st);
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace mdemi

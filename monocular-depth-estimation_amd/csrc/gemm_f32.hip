@@ -16,16 +16,24 @@
 // over workgroups into fp32 slabs reduced by a second deterministic kernel.
 //
 // Tiling: 128x128 block tile, BK = 16, 256 threads = 4 waves in 2x2, each wave
-// 64x64 = 2x2 MFMA 32x32 accumulators (64 AGPRs).  Register-staged double-
-// buffered LDS ([k][m] / [k][n] images, 32 consecutive floats per half-wave
-// fragment read: conflict-free), one barrier per K tile.
+// 64x64 = 2x2 MFMA 32x32 accumulators.  MFMA k-step s of a K tile takes, in
+// lane half h, k = 8*(s/4) + 4*h + (s%4).  Both operands are staged in LDS as
+// [k][row] images read with ds_read_b32 (32 consecutive floats per half-wave,
+// conflict-free): M/N-contiguous sources are written as float4 rows (pitch
+// 132), k-contiguous sources are transposed on the way in (4x ds_write_b32,
+// pitch 130).  Register-staged prefetch of the next K tile (issue early, write
+// late) into the second of two LDS buffers, one barrier per tile.  Block ids
+// are remapped so that the tiles an XCD runs concurrently share A row-panels
+// and B column-panels in that XCD's L2 (guide T1).  Variants: see pick_variant.
 #include "common.h"
 
 namespace mdemi {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int GBM = 128, GBN = 128, GBK = 16, GTHREADS = 256;
+constexpr int GBM = 128, GBN = 128, GTHREADS = 256;
+constexpr int PMN = GBM + 4;   // [k][row] image pitch (floats)
+template <int BK> struct PitchK { static constexpr int v = BK + 4; };  // [row][k] image pitch
 
 struct GemmParams {
   int M, N, K, batch, split, ktile_per_split;
@@ -39,17 +47,10 @@ struct GemmParams {
   float* slab;  // split-K partials [split][batch][M][N]
   mdemi_conv_geom cv;
   int a_vec, b_vec;  // 1: 16-byte vector loads legal for this operand
+  int tiles_m, tiles_n, group_m;
 };
 
-// LDS row pitch per operand layout: MN-contiguous images are written with
-// ds_write_b128 (pitch must stay 16-B aligned); K-contiguous sources are
-// transposed with 4x ds_write_b32 (pitch 130 spreads the 4 k-rows a 32-lane
-// group writes over distinct banks).
-template <int LAYOUT>
-struct Pitch { static constexpr int v = (LAYOUT == MDEMI_L_MNCONTIG) ? GBM + 4 : GBM + 2; };
-
 __device__ __forceinline__ float4 ld4_guard(const float* p, int n_valid, bool vec) {
-  // n_valid: number of leading elements inside the tensor (0..4)
   if (n_valid >= 4 && vec) return *reinterpret_cast<const float4*>(p);
   float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
   if (n_valid > 0) r.x = p[0];
@@ -65,138 +66,171 @@ __device__ __forceinline__ float4 apply_op(float4 v) {
   return v;
 }
 
+// staged-image kinds
+constexpr int IMG_RK = 0;  // [row][k], pitch PK
+constexpr int IMG_KR = 1;  // [k][row], pitch PMN (written as float4 rows)
+constexpr int IMG_KT = 2;  // [k][row], pitch GBM+2, written transposed (4x ds_write_b32) from a row-major source
+
+template <int IMG, int BK>
+struct Img {
+  static constexpr int PK = PitchK<BK>::v;
+  static constexpr int PT = (IMG == IMG_KT) ? GBM + 2 : PMN;
+  static constexpr int floats = (IMG == IMG_RK) ? GBM * PK : BK * PT;
+  // 4 consecutive MFMA k-steps (group t) for fragment row `r` of this lane half h
+  __device__ static float4 frag(const float* s, int r, int t, int h) {
+    if (IMG == IMG_RK) return *reinterpret_cast<const float4*>(s + r * PK + 8 * t + 4 * h);
+    const float* p = s + (8 * t + 4 * h) * PT + r;
+    return make_float4(p[0], p[PT], p[2 * PT], p[3 * PT]);
+  }
+};
+
 // ---------------------------------------------------------------------------
-// Operand loaders.  Each thread stages 2 float4 per operand per K tile.
-//   K-contiguous tile  (128 rows x 16 k): f = t + 256 r -> row f>>2, k-quad f&3
-//   MN-contiguous tile (16 k x 128 cols): f = t + 256 r -> k f>>5, col-quad f&31
-// `rows`/`ld`: for A rows are i (M), for B rows are j (N).
+// Operand loaders: each thread stages NQ = BK/8 float4 per operand per K tile.
+//   row-major tile  (128 rows x BK k): f = t + 256 q -> row f/(BK/4), k-quad f%(BK/4)
+//   k-major tile    (BK k x 128 cols): f = t + 256 q -> k f>>5, col-quad f&31
 // ---------------------------------------------------------------------------
-template <int LAYOUT, int OP>
+template <int BK>
+__device__ __forceinline__ void store_rk(float* lds, int t, const float4 (&r)[BK / 8]) {
+  constexpr int KQ = BK / 4, RS = 256 / KQ;
+#pragma unroll
+  for (int q = 0; q < BK / 8; ++q)
+    *reinterpret_cast<float4*>(lds + (t / KQ + RS * q) * PitchK<BK>::v + 4 * (t % KQ)) = r[q];
+}
+// row-major source tile transposed into a [k][row] image (pitch 130: the 4
+// k-rows a 32-lane group writes land on distinct banks)
+template <int BK>
+__device__ __forceinline__ void store_kt(float* lds, int t, const float4 (&r)[BK / 8]) {
+  constexpr int KQ = BK / 4, RS = 256 / KQ, P = GBM + 2;
+#pragma unroll
+  for (int q = 0; q < BK / 8; ++q) {
+    const int row = t / KQ + RS * q, k = 4 * (t % KQ);
+    lds[(k + 0) * P + row] = r[q].x;
+    lds[(k + 1) * P + row] = r[q].y;
+    lds[(k + 2) * P + row] = r[q].z;
+    lds[(k + 3) * P + row] = r[q].w;
+  }
+}
+template <int BK>
+__device__ __forceinline__ void store_kr(float* lds, int t, const float4 (&r)[BK / 8]) {
+#pragma unroll
+  for (int q = 0; q < BK / 8; ++q)
+    *reinterpret_cast<float4*>(lds + ((t >> 5) + 8 * q) * PMN + 4 * (t & 31)) = r[q];
+}
+
+template <int LAYOUT, int OP, bool IS_A, int BK, bool TR>
 struct Loader;
 
 // dense [row][k]
-template <int OP>
-struct Loader<MDEMI_L_KCONTIG, OP> {
+template <int OP, bool IS_A, int BK, bool TR>
+struct Loader<MDEMI_L_KCONTIG, OP, IS_A, BK, TR> {
+  static constexpr int IMG = TR ? IMG_KT : IMG_RK, NQ = BK / 8, KQ = BK / 4, RS = 256 / KQ;
   const float* base; int64_t ld; int rows, K; bool vec;
-  int row[2]; int kq;
-  __device__ void init(const float* p, int64_t ld_, int rows_, int K_, bool vec_, int row0, int t,
+  int row0; int kq;
+  __device__ void init(const float* p, int64_t ld_, int rows_, int K_, bool vec_, int r0, int t,
                        const mdemi_conv_geom&) {
     base = p; ld = ld_; rows = rows_; K = K_; vec = vec_;
-    row[0] = row0 + (t >> 2); row[1] = row0 + 64 + (t >> 2); kq = t & 3;
+    row0 = r0 + t / KQ; kq = t % KQ;
   }
-  __device__ void load(int k0, float4 (&r)[2]) const {
+  __device__ void load(int k0, float4 (&r)[NQ]) const {
     const int k = k0 + 4 * kq;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int nv = (row[s] < rows) ? min(4, K - k) : 0;
-      r[s] = apply_op<OP>(ld4_guard(base + (int64_t)row[s] * ld + k, nv, vec));
+    for (int q = 0; q < NQ; ++q) {
+      const int row = row0 + RS * q;
+      const int nv = (row < rows) ? min(4, K - k) : 0;
+      r[q] = apply_op<OP>(ld4_guard(base + (int64_t)row * ld + k, nv, vec));
     }
   }
-  __device__ static void store(float* lds, int t, const float4 (&r)[2]) {
-    constexpr int P = Pitch<MDEMI_L_KCONTIG>::v;
-    const int kq = t & 3;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int rl = (t >> 2) + 64 * s;
-      lds[(4 * kq + 0) * P + rl] = r[s].x;
-      lds[(4 * kq + 1) * P + rl] = r[s].y;
-      lds[(4 * kq + 2) * P + rl] = r[s].z;
-      lds[(4 * kq + 3) * P + rl] = r[s].w;
-    }
+  __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) {
+    if (TR) store_kt<BK>(lds, t, r); else store_rk<BK>(lds, t, r);
   }
 };
 
 // dense [k][row]
-template <int OP>
-struct Loader<MDEMI_L_MNCONTIG, OP> {
+template <int OP, bool IS_A, int BK, bool TR>
+struct Loader<MDEMI_L_MNCONTIG, OP, IS_A, BK, TR> {
+  static constexpr int IMG = IMG_KR, NQ = BK / 8;
   const float* base; int64_t ld; int rows, K; bool vec;
   int col; int kl;
-  __device__ void init(const float* p, int64_t ld_, int rows_, int K_, bool vec_, int row0, int t,
+  __device__ void init(const float* p, int64_t ld_, int rows_, int K_, bool vec_, int r0, int t,
                        const mdemi_conv_geom&) {
     base = p; ld = ld_; rows = rows_; K = K_; vec = vec_;
-    col = row0 + 4 * (t & 31); kl = t >> 5;
+    col = r0 + 4 * (t & 31); kl = t >> 5;
   }
-  __device__ void load(int k0, float4 (&r)[2]) const {
+  __device__ void load(int k0, float4 (&r)[NQ]) const {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int k = k0 + kl + 8 * s;
+    for (int q = 0; q < NQ; ++q) {
+      const int k = k0 + kl + 8 * q;
       const int nv = (k < K) ? min(4, rows - col) : 0;
-      r[s] = apply_op<OP>(ld4_guard(base + (int64_t)k * ld + col, nv, vec));
+      r[q] = apply_op<OP>(ld4_guard(base + (int64_t)k * ld + col, nv, vec));
     }
   }
-  __device__ static void store(float* lds, int t, const float4 (&r)[2]) {
-    constexpr int P = Pitch<MDEMI_L_MNCONTIG>::v;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-      *reinterpret_cast<float4*>(lds + ((t >> 5) + 8 * s) * P + 4 * (t & 31)) = r[s];
-  }
+  __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) { store_kr<BK>(lds, t, r); }
 };
 
-// Implicit im2col of an NHWC activation, operand A (k-contiguous role):
-// A(i, k) = X[n, oy*s - p + ky, ox*s - p + kx, c], i = (n,oy,ox), k = (ky,kx,c).
-// Requires C % 4 == 0 so a k-quad never straddles a filter tap.
-template <int OP>
-struct ConvLoaderA {
+// Implicit im2col of an NHWC activation, operand A (row = output pixel,
+// k = (ky,kx,c)).  Requires C % 4 == 0 so a k-quad never straddles a tap.
+template <int OP, int BK, bool TR>
+struct Loader<MDEMI_L_CONV, OP, true, BK, TR> {
+  static constexpr int IMG = TR ? IMG_KT : IMG_RK, NQ = BK / 8, KQ = BK / 4, RS = 256 / KQ;
   const float* base; mdemi_conv_geom g; int rows, K; int kq;
-  int n[2], iy0[2], ix0[2]; bool valid[2];
-  __device__ void init(const float* p, int64_t, int rows_, int K_, bool, int row0, int t,
-                       const mdemi_conv_geom& g_) {
-    base = p; g = g_; rows = rows_; K = K_; kq = t & 3;
+  int n[NQ], iy0[NQ], ix0[NQ]; bool valid[NQ];
+  __device__ void init(const float* p, int64_t, int rows_, int K_, bool, int r0, int t, const mdemi_conv_geom& g_) {
+    base = p; g = g_; rows = rows_; K = K_; kq = t % KQ;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int i = row0 + (t >> 2) + 64 * s;
-      valid[s] = i < rows;
-      const int ii = valid[s] ? i : 0;
+    for (int q = 0; q < NQ; ++q) {
+      const int i = r0 + t / KQ + RS * q;
+      valid[q] = i < rows;
+      const int ii = valid[q] ? i : 0;
       const int ox = ii % g.ow, tmp = ii / g.ow;
       const int oy = tmp % g.oh;
-      n[s] = tmp / g.oh;
-      iy0[s] = oy * g.stride - g.pad;
-      ix0[s] = ox * g.stride - g.pad;
+      n[q] = tmp / g.oh;
+      iy0[q] = oy * g.stride - g.pad;
+      ix0[q] = ox * g.stride - g.pad;
     }
   }
-  __device__ void load(int k0, float4 (&r)[2]) const {
+  __device__ void load(int k0, float4 (&r)[NQ]) const {
     const int k = k0 + 4 * kq;
     const bool kin = k < K;
     const int kk = kin ? k : 0;
     const int c = kk % g.c, tap = kk / g.c;
     const int kx = tap % g.kw, ky = tap / g.kw;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      int iy = iy0[s] + ky, ix = ix0[s] + kx;
-      bool ok = kin && valid[s];
+    for (int q = 0; q < NQ; ++q) {
+      int iy = iy0[q] + ky, ix = ix0[q] + kx;
+      bool ok = kin && valid[q];
       if (g.pad_mode == MDEMI_PAD_REPLICATE) {
         iy = min(max(iy, 0), g.h - 1); ix = min(max(ix, 0), g.w - 1);
       } else {
         ok = ok && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
       }
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) v = *reinterpret_cast<const float4*>(base + (((int64_t)n[s] * g.h + iy) * g.w + ix) * g.c + c);
-      r[s] = apply_op<OP>(v);
+      if (ok) v = *reinterpret_cast<const float4*>(base + (((int64_t)n[q] * g.h + iy) * g.w + ix) * g.c + c);
+      r[q] = apply_op<OP>(v);
     }
   }
-  __device__ static void store(float* lds, int t, const float4 (&r)[2]) {
-    Loader<MDEMI_L_KCONTIG, OP>::store(lds, t, r);
+  __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) {
+    if (TR) store_kt<BK>(lds, t, r); else store_rk<BK>(lds, t, r);
   }
 };
 
-// Implicit im2col, operand B (n-contiguous role, weight gradients):
-// B(k, j) = X[n, oy*s - p + ky, ox*s - p + kx, c], k = (n,oy,ox), j = (ky,kx,c).
-template <int OP>
-struct ConvLoaderB {
+// Implicit im2col, operand B (weight gradients): B(k, j) with k = output pixel,
+// j = (ky,kx,c); staged k-major like a dense [k][col] operand.
+template <int OP, int BK, bool TR>
+struct Loader<MDEMI_L_CONV, OP, false, BK, TR> {
+  static constexpr int IMG = IMG_KR, NQ = BK / 8;
   const float* base; mdemi_conv_geom g; int cols, K; int kl;
   int c, ky, kx; bool jvalid;
-  __device__ void init(const float* p, int64_t, int cols_, int K_, bool, int col0, int t,
-                       const mdemi_conv_geom& g_) {
+  __device__ void init(const float* p, int64_t, int cols_, int K_, bool, int c0, int t, const mdemi_conv_geom& g_) {
     base = p; g = g_; cols = cols_; K = K_; kl = t >> 5;
-    const int j = col0 + 4 * (t & 31);
+    const int j = c0 + 4 * (t & 31);
     jvalid = j < cols;
     const int jj = jvalid ? j : 0;
     c = jj % g.c; const int tap = jj / g.c; kx = tap % g.kw; ky = tap / g.kw;
   }
-  __device__ void load(int k0, float4 (&r)[2]) const {
+  __device__ void load(int k0, float4 (&r)[NQ]) const {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int k = k0 + kl + 8 * s;
+    for (int q = 0; q < NQ; ++q) {
+      const int k = k0 + kl + 8 * q;
       bool ok = jvalid && k < K;
       const int kk = ok ? k : 0;
       const int ox = kk % g.ow, tmp = kk / g.ow;
@@ -209,27 +243,10 @@ struct ConvLoaderB {
       }
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (ok) v = *reinterpret_cast<const float4*>(base + (((int64_t)nn * g.h + iy) * g.w + ix) * g.c + c);
-      r[s] = apply_op<OP>(v);
+      r[q] = apply_op<OP>(v);
     }
   }
-  __device__ static void store(float* lds, int t, const float4 (&r)[2]) {
-    Loader<MDEMI_L_MNCONTIG, OP>::store(lds, t, r);
-  }
-};
-
-template <int LAYOUT, int OP, bool IS_A>
-struct PickLoader { using T = Loader<LAYOUT, OP>; };
-template <int OP>
-struct PickLoader<MDEMI_L_CONV, OP, true> { using T = ConvLoaderA<OP>; };
-template <int OP>
-struct PickLoader<MDEMI_L_CONV, OP, false> { using T = ConvLoaderB<OP>; };
-
-// LDS pitch of the staged image: the conv A loader writes like a K-contiguous
-// operand, the conv B loader like an MN-contiguous one.
-template <int LAYOUT, bool IS_A>
-struct StagePitch {
-  static constexpr int v = (LAYOUT == MDEMI_L_CONV) ? (IS_A ? Pitch<MDEMI_L_KCONTIG>::v : Pitch<MDEMI_L_MNCONTIG>::v)
-                                                    : Pitch<LAYOUT>::v;
+  __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) { store_kr<BK>(lds, t, r); }
 };
 
 __device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int i, int j, float acc) {
@@ -243,25 +260,55 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int 
   return v;
 }
 
-template <int AL, int BL, int AOP, int BOP>
+// tile (tm, tn) for a linear workgroup id: XCD-aware remap (blocks b, b+8, ...
+// share an XCD), then grouped raster so concurrently running tiles of one XCD
+// reuse A row-panels (group_m rows of tiles) and B column-panels.
+__device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles, int& tm, int& tn) {
+  if (p.group_m <= 0) {  // plain raster: n fastest
+    tm = bid / p.tiles_n;
+    tn = bid % p.tiles_n;
+    return;
+  }
+  const int q = ntiles / 8, r = ntiles % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  const int per_group = p.group_m * p.tiles_n;
+  const int grp = lin / per_group;
+  const int first_m = grp * p.group_m;
+  const int gm = min(p.tiles_m - first_m, p.group_m);
+  const int in_grp = lin % per_group;
+  tm = first_m + in_grp % gm;
+  tn = in_grp / gm;
+}
+
+// Pipelining variants (A/B-tested on the model's shapes, tools/gemm_bench.py):
+//   BK    K depth per LDS tile (16 or 32)
+//   NBUF  LDS buffers (2: write the next tile while others read this one)
+//   PREF  register prefetch of the next tile before the MFMAs (issue early / write late)
+template <int AL, int BL, int AOP, int BOP, int BK, int NBUF, bool PREF, bool TR>
 __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(GemmParams p) {
-  constexpr int PA = StagePitch<AL, true>::v;
-  constexpr int PB = StagePitch<BL, false>::v;
-  __shared__ __attribute__((aligned(16))) float As[2][GBK * PA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][GBK * PB];
+  using LA = Loader<AL, AOP, true, BK, TR>;
+  using LB = Loader<BL, BOP, false, BK, TR>;
+  constexpr int FA = Img<LA::IMG, BK>::floats, FB = Img<LB::IMG, BK>::floats;
+  constexpr int NQ = BK / 8;
+  static_assert(NBUF == 2 || NBUF == 1, "NBUF");
+  __shared__ __attribute__((aligned(16))) float smem[NBUF * (FA + FB)];
 
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int zb = blockIdx.z;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int zb = blockIdx.x / ntiles;
+  int tm, tn;
+  tile_of(p, blockIdx.x % ntiles, ntiles, tm, tn);
   const int b = zb / p.split, sidx = zb % p.split;
-  const int bm = blockIdx.y * GBM, bn = blockIdx.x * GBN;
+  const int bm = tm * GBM, bn = tn * GBN;
 
-  typename PickLoader<AL, AOP, true>::T la;
-  typename PickLoader<BL, BOP, false>::T lb;
+  LA la;
+  LB lb;
   la.init(p.A + (int64_t)b * p.a_bs, p.lda, p.M, p.K, p.a_vec, bm, t, p.cv);
   lb.init(p.B + (int64_t)b * p.b_bs, p.ldb, p.N, p.K, p.b_vec, bn, t, p.cv);
 
-  const int ktiles_total = (p.K + GBK - 1) / GBK;
+  const int ktiles_total = (p.K + BK - 1) / BK;
   const int kt_begin = sidx * p.ktile_per_split;
   const int kt_end = min(ktiles_total, kt_begin + p.ktile_per_split);
 
@@ -273,43 +320,60 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
 
-  float4 ra[2], rb[2];
-  int cur = 0;
-  if (kt_begin < kt_end) {
-    la.load(kt_begin * GBK, ra);
-    lb.load(kt_begin * GBK, rb);
-    la.store(As[0], t, ra);
-    lb.store(Bs[0], t, rb);
-  }
-  __syncthreads();
-
+  float4 ra[NQ], rb[NQ];
   const int l31 = lane & 31, h = lane >> 5;
+  const int ra0 = wm * 64 + l31, ra1 = ra0 + 32;
+  const int rb0 = wn * 64 + l31, rb1 = rb0 + 32;
+
+  if (PREF && kt_begin < kt_end) {
+    la.load(kt_begin * BK, ra);
+    lb.load(kt_begin * BK, rb);
+    LA::store(smem, t, ra);
+    LB::store(smem + FA, t, rb);
+    __syncthreads();
+  }
+
+  int cur = 0;
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const bool more = kt + 1 < kt_end;
-    if (more) {
-      la.load((kt + 1) * GBK, ra);
-      lb.load((kt + 1) * GBK, rb);
+    if (!PREF) {  // plain: load, stage, barrier, compute (other workgroups overlap)
+      la.load(kt * BK, ra);
+      lb.load(kt * BK, rb);
+      LA::store(smem, t, ra);
+      LB::store(smem + FA, t, rb);
+      __syncthreads();
+    } else if (more) {  // issue next tile's global loads early; they land under the MFMAs
+      la.load((kt + 1) * BK, ra);
+      lb.load((kt + 1) * BK, rb);
     }
-    const float* a_s = As[cur];
-    const float* b_s = Bs[cur];
+    const float* a_s = smem + cur * (FA + FB);
+    const float* b_s = a_s + FA;
 #pragma unroll
-    for (int kk = 0; kk < GBK / 2; ++kk) {
-      const int krow = 2 * kk + h;
-      const float a0 = a_s[krow * PA + wm * 64 + l31];
-      const float a1 = a_s[krow * PA + wm * 64 + 32 + l31];
-      const float b0 = b_s[krow * PB + wn * 64 + l31];
-      const float b1 = b_s[krow * PB + wn * 64 + 32 + l31];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    for (int g = 0; g < BK / 8; ++g) {
+      const float4 a0 = Img<LA::IMG, BK>::frag(a_s, ra0, g, h);
+      const float4 a1 = Img<LA::IMG, BK>::frag(a_s, ra1, g, h);
+      const float4 b0 = Img<LB::IMG, BK>::frag(b_s, rb0, g, h);
+      const float4 b1 = Img<LB::IMG, BK>::frag(b_s, rb1, g, h);
+#define MDEMI_STEP(X)                                                                  \
+  acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.X, b0.X, acc[0][0], 0, 0, 0); \
+  acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.X, b1.X, acc[0][1], 0, 0, 0); \
+  acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.X, b0.X, acc[1][0], 0, 0, 0); \
+  acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.X, b1.X, acc[1][1], 0, 0, 0);
+      MDEMI_STEP(x) MDEMI_STEP(y) MDEMI_STEP(z) MDEMI_STEP(w)
+#undef MDEMI_STEP
     }
-    if (more) {
-      la.store(As[cur ^ 1], t, ra);
-      lb.store(Bs[cur ^ 1], t, rb);
+    if (!PREF) {
+      __syncthreads();
+    } else {
+      if (more) {
+        if (NBUF == 1) __syncthreads();  // everyone done reading before overwrite
+        float* dst = smem + (NBUF == 1 ? 0 : (cur ^ 1)) * (FA + FB);
+        LA::store(dst, t, ra);
+        LB::store(dst + FA, t, rb);
+      }
+      __syncthreads();
+      if (NBUF == 2) cur ^= 1;
     }
-    __syncthreads();
-    cur ^= 1;
   }
 
   // Epilogue.  acc[tm][tn][r] holds C(row, col) with
@@ -317,30 +381,30 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(GemmParams p) {
   if (p.split > 1) {
     float* S = p.slab + ((int64_t)sidx * p.batch + b) * (int64_t)p.M * p.N;
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int im = 0; im < 2; ++im)
 #pragma unroll
-      for (int tn = 0; tn < 2; ++tn) {
-        const int j = bn + wn * 64 + tn * 32 + l31;
+      for (int in = 0; in < 2; ++in) {
+        const int j = bn + wn * 64 + in * 32 + l31;
         if (j >= p.N) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int i = bm + wm * 64 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (i < p.M) S[(int64_t)i * p.N + j] = acc[tm][tn][r];
+          const int i = bm + wm * 64 + im * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (i < p.M) S[(int64_t)i * p.N + j] = acc[im][in][r];
         }
       }
     return;
   }
   float* Cb = p.C + (int64_t)b * p.c_bs;
 #pragma unroll
-  for (int tm = 0; tm < 2; ++tm)
+  for (int im = 0; im < 2; ++im)
 #pragma unroll
-    for (int tn = 0; tn < 2; ++tn) {
-      const int j = bn + wn * 64 + tn * 32 + l31;
+    for (int in = 0; in < 2; ++in) {
+      const int j = bn + wn * 64 + in * 32 + l31;
       if (j >= p.N) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int i = bm + wm * 64 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (i < p.M) Cb[(int64_t)i * p.ldc + j] = epilogue_value(p, b, i, j, acc[tm][tn][r]);
+        const int i = bm + wm * 64 + im * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (i < p.M) Cb[(int64_t)i * p.ldc + j] = epilogue_value(p, b, i, j, acc[im][in][r]);
       }
     }
 }
@@ -362,19 +426,40 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
 
 using KernelFn = void (*)(GemmParams);
 
+// Variant table (benchmark hook mdemi_gemm_set_variant).  Measured on the
+// NewCRFs-L07 480x640 bs=8 shapes (tools/gemm_bench.py, profiles/r01_gemm_variants.log):
+//   BK16/NBUF2/prefetch with k-contiguous operands TRANSPOSED into [k][row]
+//   images (ds_read_b32 fragments) 80 TF; the same with [row][k] images and
+//   ds_read_b128 fragments 69 TF; BK32 (2 LDS buffers) 58 TF (VGPRs 170 ->
+//   2 waves/SIMD); BK32 single buffer 64-73 TF; plain load/barrier/compute
+//   BK16 75-79 TF.  XCD-grouped raster vs plain: +0.5 TF.
+//   0 (default): BK16 NBUF2 PREF transposed     1: BK16 NBUF2 PREF [row][k]
+static int g_variant = 0;
+static int g_group_m = 8;
+
+template <int AL, int BL, int AOP, int BOP>
+static KernelFn pick_variant(int v) {
+  switch (v) {
+    case 1: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, false>;
+    default: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true>;
+  }
+}
+
 template <int AL, int BL>
-static KernelFn pick_ops(int aop, int bop) {
-  if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_NONE) return gemm_f32_kernel<AL, BL, MDEMI_OP_NONE, MDEMI_OP_NONE>;
-  if (aop == MDEMI_OP_GELU && bop == MDEMI_OP_NONE && AL == MDEMI_L_KCONTIG)
-    return gemm_f32_kernel<AL, BL, MDEMI_OP_GELU, MDEMI_OP_NONE>;
-  if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_GELU && BL == MDEMI_L_MNCONTIG)
-    return gemm_f32_kernel<AL, BL, MDEMI_OP_NONE, MDEMI_OP_GELU>;
+static KernelFn pick_ops(int aop, int bop, int v) {
+  if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_NONE) return pick_variant<AL, BL, MDEMI_OP_NONE, MDEMI_OP_NONE>(v);
+  if constexpr (AL == MDEMI_L_KCONTIG)
+    if (aop == MDEMI_OP_GELU && bop == MDEMI_OP_NONE)
+      return pick_variant<AL, BL, MDEMI_OP_GELU, MDEMI_OP_NONE>(v);
+  if constexpr (BL == MDEMI_L_MNCONTIG)
+    if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_GELU)
+      return pick_variant<AL, BL, MDEMI_OP_NONE, MDEMI_OP_GELU>(v);
   return nullptr;
 }
 
-static KernelFn pick_kernel(int al, int bl, int aop, int bop) {
+static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
 #define MDEMI_PICK(X, Y) \
-  if (al == X && bl == Y) return pick_ops<X, Y>(aop, bop);
+  if (al == X && bl == Y) return pick_ops<X, Y>(aop, bop, v);
   MDEMI_PICK(MDEMI_L_KCONTIG, MDEMI_L_KCONTIG)
   MDEMI_PICK(MDEMI_L_KCONTIG, MDEMI_L_MNCONTIG)
   MDEMI_PICK(MDEMI_L_MNCONTIG, MDEMI_L_KCONTIG)
@@ -386,6 +471,8 @@ static KernelFn pick_kernel(int al, int bl, int aop, int bop) {
 #undef MDEMI_PICK
   return nullptr;
 }
+
+static int variant_bk(int) { return 16; }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -415,6 +502,7 @@ static int validate(const mdemi_gemm_desc* d) {
 }
 
 static void fill_params(const mdemi_gemm_desc* d, GemmParams& p) {
+  const int GBK = variant_bk(g_variant);
   p.M = d->M; p.N = d->N; p.K = d->K; p.batch = d->batch;
   p.A = d->A; p.lda = d->lda; p.a_bs = d->a_bstride;
   p.B = d->B; p.ldb = d->ldb; p.b_bs = d->b_bstride;
@@ -432,6 +520,9 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p) {
   p.a_vec = al16(d->A) && (d->lda % 4 == 0) && (d->a_bstride % 4 == 0);
   p.b_vec = al16(d->B) && (d->ldb % 4 == 0) && (d->b_bstride % 4 == 0);
   p.slab = nullptr;
+  p.tiles_m = (int)cdiv(d->M, GBM);
+  p.tiles_n = (int)cdiv(d->N, GBN);
+  p.group_m = g_group_m;
 }
 
 }  // namespace mdemi
@@ -449,7 +540,7 @@ extern "C" size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d) {
 extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {
   int rc = validate(d);
   if (rc) return rc;
-  KernelFn fn = pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op);
+  KernelFn fn = pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, g_variant);
   if (!fn) {
     set_error("gemm: unsupported layout/op combination a=%d/%d b=%d/%d", d->a_layout, d->a_op, d->b_layout,
               d->b_op);
@@ -466,13 +557,22 @@ extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {
     p.slab = (float*)d->workspace;
   }
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid((unsigned)cdiv(d->N, GBN), (unsigned)cdiv(d->M, GBM), (unsigned)(d->batch * p.split));
-  MDEMI_REQUIRE(grid.y <= 65535 && grid.z <= 65535, "gemm: grid too large");
-  hipLaunchKernelGGL(fn, grid, dim3(GTHREADS), 0, st, p);
+  const int64_t nblocks = (int64_t)p.tiles_m * p.tiles_n * d->batch * p.split;
+  MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
+  hipLaunchKernelGGL(fn, dim3((unsigned)nblocks), dim3(GTHREADS), 0, st, p);
   if (p.split > 1) {
     const int64_t total = (int64_t)d->M * d->N * d->batch;
     const int nb = (int)(cdiv(total, 256) < 4096 ? cdiv(total, 256) : 4096);
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(nb), dim3(256), 0, st, p);
   }
   return check_launch("gemm_f32");
+}
+
+// Benchmark/tuning hook: select the pipelining variant (see pick_variant) and
+// the tile raster (group_m > 0: XCD-aware grouped raster; 0: plain).
+extern "C" int mdemi_gemm_set_variant(int32_t variant, int32_t group_m) {
+  MDEMI_REQUIRE(variant >= 0 && variant <= 1 && group_m >= 0, "gemm_set_variant: bad args");
+  g_variant = variant;
+  g_group_m = group_m;
+  return MDEMI_OK;
 }

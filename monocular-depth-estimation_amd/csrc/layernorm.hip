@@ -148,14 +148,12 @@ __global__ __launch_bounds__(LN_THREADS) void ln_bwd_kernel(const float* __restr
   }
 }
 
-__global__ void ln_param_reduce(const float* __restrict__ partial, float* __restrict__ dgamma,
-                                float* __restrict__ dbeta, int nblk, int C) {
+__global__ void ln_param_split(const float* __restrict__ sums, float* __restrict__ dgamma, float* __restrict__ dbeta,
+                               int C) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * C) return;
-  float s = 0.f;
-  for (int i = 0; i < nblk; ++i) s += partial[(int64_t)i * 2 * C + c];
-  if (c < C) { if (dgamma) dgamma[c] = s; }
-  else if (dbeta) dbeta[c - C] = s;
+  if (c >= C) return;
+  if (dgamma) dgamma[c] = sums[c];
+  if (dbeta) dbeta[c] = sums[C + c];
 }
 
 static int ln_cache(int C) {
@@ -204,8 +202,10 @@ extern "C" int mdemi_layernorm_fwd(const float* x, const float* gamma, const flo
   return check_launch("layernorm_fwd");
 }
 
+// workspace: [partials nb x 2C | sums 2C | colsum scratch]
+static size_t ln_part_bytes(int64_t rows, int C) { return align_up((size_t)ln_bwd_blocks(rows, C) * 2 * C * 4, 256); }
 extern "C" size_t mdemi_layernorm_bwd_workspace_size(int64_t rows, int32_t C) {
-  return (size_t)ln_bwd_blocks(rows, C) * 2 * C * sizeof(float);
+  return ln_part_bytes(rows, C) + align_up((size_t)2 * C * 4, 256) + colsum_ws_bytes(ln_bwd_blocks(rows, C), 2 * C);
 }
 
 extern "C" int mdemi_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
@@ -221,6 +221,12 @@ extern "C" int mdemi_layernorm_bwd(const float* dy, const float* x, const float*
   float* partial = (float*)workspace;
   LN_DISPATCH(cache, ln_bwd_kernel, dim3(nb), dim3(LN_THREADS), 0, st, dy, x, mean, rstd, gamma, dx, partial, rows,
               C, accumulate_dx);
-  hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 255) / 256), dim3(256), 0, st, partial, dgamma, dbeta, nb, C);
+  if (dgamma || dbeta) {
+    float* sums = (float*)((char*)workspace + ln_part_bytes(rows, C));
+    void* cws = (char*)sums + align_up((size_t)2 * C * 4, 256);
+    int rc = colsum_launch(partial, nb, 2 * C, 2 * C, sums, 0, cws, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(ln_param_split, dim3((C + 255) / 256), dim3(256), 0, st, sums, dgamma, dbeta, C);
+  }
   return check_launch("layernorm_bwd");
 }

@@ -158,22 +158,29 @@ extern "C" int mdemi_elementwise(int32_t op, const float* a, const float* b, flo
   return check_launch("elementwise");
 }
 
-extern "C" size_t mdemi_colsum_workspace_size(int64_t rows, int64_t cols) {
-  return (size_t)colsum_blocks_y(rows) * cols * sizeof(float);
+namespace mdemi {
+size_t colsum_ws_bytes(int64_t rows, int64_t cols) {
+  return align_up((size_t)colsum_blocks_y(rows) * cols * sizeof(float), 256);
 }
+int colsum_launch(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, int accumulate, void* ws,
+                  hipStream_t st) {
+  const int ny = colsum_blocks_y(rows);
+  const int64_t rpb = cdiv(rows, ny);
+  dim3 grid((unsigned)cdiv(cols, 32), (unsigned)ny);
+  hipLaunchKernelGGL(colsum_partial, grid, dim3(256), 0, st, x, rows, cols, ld, (float*)ws, rpb);
+  hipLaunchKernelGGL(colsum_final, dim3((unsigned)cdiv(cols, 256)), dim3(256), 0, st, (const float*)ws, ny, cols, out,
+                     accumulate);
+  return check_launch("colsum");
+}
+}  // namespace mdemi
+
+extern "C" size_t mdemi_colsum_workspace_size(int64_t rows, int64_t cols) { return colsum_ws_bytes(rows, cols); }
 
 extern "C" int mdemi_colsum_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, int accumulate,
                                 void* workspace, void* stream) {
   MDEMI_REQUIRE(x && out && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
   if (!workspace) { set_error("colsum: workspace required"); return MDEMI_EWORKSPACE; }
-  hipStream_t st = (hipStream_t)stream;
-  const int ny = colsum_blocks_y(rows);
-  const int64_t rpb = cdiv(rows, ny);
-  dim3 grid((unsigned)cdiv(cols, 32), (unsigned)ny);
-  hipLaunchKernelGGL(colsum_partial, grid, dim3(256), 0, st, x, rows, cols, ld, (float*)workspace, rpb);
-  hipLaunchKernelGGL(colsum_final, dim3((unsigned)cdiv(cols, 256)), dim3(256), 0, st, (const float*)workspace, ny,
-                     cols, out, accumulate);
-  return check_launch("colsum");
+  return colsum_launch(x, rows, cols, ld, out, accumulate, workspace, (hipStream_t)stream);
 }
 
 // Workspace layout for the optimizer entry points (host computes chunk maps):

@@ -292,16 +292,16 @@ __global__ __launch_bounds__(64) void winattn_bwd_kernel(WinParams p) {
   if (lane < HD) { P[T + lane] = padk[lane]; P[T + HD + lane] = padv[lane]; }
 }
 
-// d_rpb_table[t][h] = sum_win partial[win][h][t]; dk_pad / dv_pad likewise.
+// sums[h][t] (column sums over windows of partial[win][h][T + 2*HD]) ->
+// d_rpb_table[t][h], dk_pad / dv_pad [h*HD + d]
 template <int WS, int HD>
-__global__ void winattn_bwd_reduce(const float* __restrict__ partial, int nwin, int heads, float* d_rpb,
-                                   float* dk_pad, float* dv_pad, float* dq_pad) {
+__global__ void winattn_bwd_scatter(const float* __restrict__ sums, int heads, float* d_rpb, float* dk_pad,
+                                    float* dv_pad, float* dq_pad) {
   constexpr int T = (2 * WS - 1) * (2 * WS - 1), R = T + 2 * HD;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= heads * R) return;
   const int h = e / R, t = e % R;
-  float s = 0.f;
-  for (int w = 0; w < nwin; ++w) s += partial[((int64_t)w * heads + h) * R + t];
+  const float s = sums[e];
   if (t < T) d_rpb[t * heads + h] = s;
   else if (t < T + HD) { if (dk_pad) dk_pad[h * HD + t - T] = s; }
   else if (dv_pad) dv_pad[h * HD + t - T - HD] = s;
@@ -346,12 +346,15 @@ extern "C" int mdemi_winattn_fwd(const mdemi_winattn_desc* d, void* stream) {
   return check_launch("winattn_fwd");
 }
 
+// workspace: [partials nwin x heads*R | sums heads*R | colsum scratch]
+static size_t wa_part_bytes(int nwin, int heads, int R) { return align_up((size_t)nwin * heads * R * 4, 256); }
 extern "C" size_t mdemi_winattn_bwd_workspace_size(const mdemi_winattn_desc* d) {
   WinParams p;
   int nwin;
   if (make_params(d, p, nwin)) return 0;
-  const int T = (2 * d->window - 1) * (2 * d->window - 1);
-  return (size_t)nwin * d->heads * (T + 2 * d->head_dim) * sizeof(float);
+  const int R = (2 * d->window - 1) * (2 * d->window - 1) + 2 * d->head_dim;
+  return wa_part_bytes(nwin, d->heads, R) + align_up((size_t)d->heads * R * 4, 256) +
+         colsum_ws_bytes(nwin, (int64_t)d->heads * R);
 }
 
 extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
@@ -369,7 +372,11 @@ extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL((winattn_bwd_kernel<7, 32>), dim3(nwin, d->heads), dim3(64), 0, st, p);
   const int R = 13 * 13 + 64;
-  hipLaunchKernelGGL((winattn_bwd_reduce<7, 32>), dim3((d->heads * R + 255) / 256), dim3(256), 0, st, p.partial, nwin,
-                     d->heads, d->d_rpb_table, d->dk_pad, d->dv_pad, d->dq_pad);
+  float* sums = (float*)((char*)d->workspace + wa_part_bytes(nwin, d->heads, R));
+  void* cws = (char*)sums + align_up((size_t)d->heads * R * 4, 256);
+  int rc2 = colsum_launch(p.partial, nwin, (int64_t)d->heads * R, (int64_t)d->heads * R, sums, 0, cws, st);
+  if (rc2) return rc2;
+  hipLaunchKernelGGL((winattn_bwd_scatter<7, 32>), dim3((d->heads * R + 255) / 256), dim3(256), 0, st, sums, d->heads,
+                     d->d_rpb_table, d->dk_pad, d->dv_pad, d->dq_pad);
   return check_launch("winattn_bwd");
 }

@@ -18,7 +18,7 @@ import threading
 import torch  # noqa: F401  (must be imported before the HIP library is mapped)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmdemi.so")
+LIB_PATH = os.environ.get("MDEMI_LIB") or os.path.join(_HERE, "libmdemi.so")  # override: A/B benchmarking
 HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "mdemi.h"))
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -93,6 +93,7 @@ _SIGS = {
     "mdemi_version": (ctypes.c_int, []),
     "mdemi_gemm_workspace_size": (sz, [ctypes.POINTER(GemmDesc)]),
     "mdemi_gemm_f32": (ctypes.c_int, [ctypes.POINTER(GemmDesc), vp]),
+    "mdemi_gemm_set_variant": (ctypes.c_int, [i32, i32]),
     "mdemi_colsum_workspace_size": (sz, [i64, i64]),
     "mdemi_colsum_f32": (ctypes.c_int, [vp, i64, i64, i64, vp, ctypes.c_int, vp, vp]),
     "mdemi_headconv_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
@@ -155,7 +156,11 @@ def load():
                 "`make -C monocular-depth-estimation_amd/csrc` (or __graft_entry__.build())")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                if os.environ.get("MDEMI_LIB"):  # an A/B build of an older ABI
+                    continue
+                raise MdemiLibraryError(f"{LIB_PATH} does not export {name}")
             fn.restype = res
             fn.argtypes = args
         _lib = lib
