@@ -173,7 +173,9 @@ typedef struct mdemi_winattn_desc {
   const float* q_pad; const float* k_pad;
   const float* v; int64_t v_ld; const float* v_pad;
   const float* rpb_table;          /* [(2w-1)^2][heads] */
-  float* out; int64_t out_ld;
+  float* out; int64_t out_ld;     /* forward output; the backward reads it (D = rowsum(dO*O)) */
+  float* lse;                      /* [nwin][heads][window^2] row log-sum-exp: written by the
+                                      forward (may be NULL there), required by the backward */
   /* backward only */
   const float* dout;
   float* dq; float* dk; int64_t dqk_ld;

@@ -55,13 +55,27 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// Exact-erf GELU (nn.GELU default) via Abramowitz & Stegun 7.1.26:
+// erfc(z) = t(a1 + t(a2 + t(a3 + t(a4 + t a5)))) e^{-z^2}, t = 1/(1 + p z), |err| <= 1.5e-7,
+// branch-free; Phi(x) is formed without cancellation for x < 0 and the
+// e^{-x^2/2} factor is shared with GELU'(x) = Phi(x) + x phi(x).
+__device__ __forceinline__ float gelu_cdf(float x, float& e) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  e = __expf(-z * z);
+  const float half_erfc = 0.5f * poly * e;
+  return x >= 0.f ? 1.f - half_erfc : half_erfc;
+}
 __device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  float e;
+  return x * gelu_cdf(x, e);
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float e;
+  const float cdf = gelu_cdf(x, e);
+  return fmaf(x * 0.39894228040143268f, e, cdf);
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
 

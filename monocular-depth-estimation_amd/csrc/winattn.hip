@@ -16,9 +16,11 @@
 // (px+s)%Wp); it is a pad token when oy>=H or ox>=W.  The mask region of a
 // rolled-padded coordinate is 0 / 1 / 2 for [0,Hp-WS) / [Hp-WS,Hp-s) / [Hp-s,Hp).
 //
-// Work per (window, head) is 2*N*N*HD FMAs with N = 49: small, so the kernel is
-// VALU + LDS-broadcast (lane = query token, K/V rows broadcast from LDS); the
-// score row lives in registers (N compile-time).
+// Work per (window, head) is 2*N*N*HD FMAs with N = 49: small (fp32 MFMA has
+// the same FLOP rate as the f32 VALU and 49 pads to 64), so the kernels are
+// VALU + LDS-broadcast (lane = token, the other side's rows broadcast from
+// LDS); the forward keeps the score row in registers (N compile-time) and
+// saves each row's log-sum-exp for the backward.
 #include "common.h"
 
 namespace mdemi {
@@ -82,10 +84,12 @@ struct WinParams {
   const float* v; int64_t v_ld; const float* v_pad;
   const float* rpb;
   float* out; int64_t out_ld;
+  float* lse;  // [nwin][heads][N] log-sum-exp of each score row (+inf for pad queries)
   const float* dout;
   float* dq; float* dk; int64_t dqk_ld;
   float* dv; int64_t dv_ld;
   float* partial;  // [nwin][heads][T + 2*HD]
+  float* dsum;     // [nwin][heads][N]  D_i = dO_i . O_i
 };
 
 template <int WS, int HD>
@@ -109,7 +113,11 @@ __global__ __launch_bounds__(64) void winattn_fwd_kernel(WinParams p) {
   const int i = lane;
   if (i >= N) return;
   const int ri = w.row(g, i);
-  if (ri < 0) return;  // pad query: its output is cropped away
+  float* lse_row = p.lse ? p.lse + ((int64_t)win * g.heads + h) * N : nullptr;
+  if (ri < 0) {  // pad query: its output is cropped away
+    if (lse_row) lse_row[i] = INFINITY;
+    return;
+  }
   const int reg_i = g.shift > 0 ? w.region(g, i) : 0;
   float4 q[H4];
   load_row<HD>(q, p.q + (int64_t)ri * p.qk_ld + h * HD);
@@ -131,6 +139,7 @@ __global__ __launch_bounds__(64) void winattn_fwd_kernel(WinParams p) {
 #pragma unroll
   for (int j = 0; j < N; ++j) { s[j] = __expf(s[j] - m); l += s[j]; }
   const float inv = 1.f / l;
+  if (lse_row) lse_row[i] = m + __logf(l);
   float4 o[H4];
 #pragma unroll
   for (int c = 0; c < H4; ++c) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -149,88 +158,66 @@ __global__ __launch_bounds__(64) void winattn_fwd_kernel(WinParams p) {
   for (int c = 0; c < H4; ++c) dst[c] = o[c];
 }
 
-// Backward (one (window, head) per workgroup, 64 lanes).
-// Phase A (lane = query i): recompute the score row into LDS, softmax it in
-//   place (P), dP_ij = dO_i . v_j, D_i = sum_j P_ij dP_ij,
-//   dS_ij = P_ij (dP_ij - D_i), dQ_i = scale * sum_j dS_ij k_j, and the bias-table
-//   gradient through LDS atomics.  P and dS stay in LDS ([N][N], odd pitch:
-//   lane-row accesses are bank-conflict free).
-// Phase B (lane = key j): dK_j = sum_i dS_ij (scale q_i), dV_j = sum_i P_ij dO_i,
-//   with the K/V staging area reused for scale*Q and dO.  Pad keys add into
-//   per-window pad sums (their q/k/v came from the Linear's bias).
+// Backward, split by role so each kernel stages only 2 row-sets in LDS
+// (~13 KB: ~3 waves/SIMD instead of 1) and keeps no score matrix:
+//   P_ij = exp(S_ij - lse_i) from the forward's saved log-sum-exp,
+//   D_i = dO_i . O_i (the identity rowsum(P o dP) = dO . O), dS = P (dP - D).
+// Q-kernel (lane = query i, K/V rows in LDS): dQ_i = scale * sum_j dS_ij k_j,
+//   bias-table gradient through LDS atomics, D_i for the KV-kernel.
+// KV-kernel (lane = key j, scale*Q / dO rows in LDS): dK_j = sum_i dS_ij (scale q_i),
+//   dV_j = sum_i P_ij dO_i; pad keys add into per-window pad sums.
 template <int WS, int HD>
-__global__ __launch_bounds__(64) void winattn_bwd_kernel(WinParams p) {
+__global__ __launch_bounds__(64) void winattn_bwd_q_kernel(WinParams p) {
   constexpr int N = WS * WS, T = (2 * WS - 1) * (2 * WS - 1), H4 = HD / 4;
-  constexpr int NP = N | 1;  // odd pitch
-  __shared__ float4 KQ[N][H4];  // K in phase A, scale*Q in phase B
-  __shared__ float4 VD[N][H4];  // V in phase A, dO in phase B
-  __shared__ float Ps[N * NP];
-  __shared__ float dSs[N * NP];
+  __shared__ float4 Ks[N][H4];
+  __shared__ float4 Vs[N][H4];
   __shared__ float tab[T];
   __shared__ float tabg[T];
-  __shared__ float padk[HD], padv[HD];
   const WinGeom& g = p.g;
   const int win = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
   const Win<WS> w(g, win);
   for (int e = lane; e < N * H4; e += 64) {
     const int j = e / H4, q4 = e % H4;
     const int r = w.row(g, j);
-    KQ[j][q4] = ld_tok4(p.k, p.qk_ld, r, p.k_pad, h * HD + 4 * q4);
-    VD[j][q4] = ld_tok4(p.v, p.v_ld, r, p.v_pad, h * HD + 4 * q4);
+    Ks[j][q4] = ld_tok4(p.k, p.qk_ld, r, p.k_pad, h * HD + 4 * q4);
+    Vs[j][q4] = ld_tok4(p.v, p.v_ld, r, p.v_pad, h * HD + 4 * q4);
   }
   for (int e = lane; e < T; e += 64) { tab[e] = p.rpb[e * g.heads + h]; tabg[e] = 0.f; }
-  if (lane < HD) { padk[lane] = 0.f; padv[lane] = 0.f; }
   __syncthreads();
-
   const int i = lane;
-  const int ri = i < N ? w.row(g, i) : -1;
-  float4 q[H4], dO[H4];
+  const int64_t rowbase = ((int64_t)win * g.heads + h) * N;
   if (i < N) {
-    float* Prow = Ps + i * NP;
-    float* Srow = dSs + i * NP;
+    const int ri = w.row(g, i);
     if (ri >= 0) {
       const int reg_i = g.shift > 0 ? w.region(g, i) : 0;
+      float4 q[H4], dO[H4];
       load_row<HD>(q, p.q + (int64_t)ri * p.qk_ld + h * HD);
-#pragma unroll
-      for (int c = 0; c < H4; ++c) { q[c].x *= p.scale; q[c].y *= p.scale; q[c].z *= p.scale; q[c].w *= p.scale; }
       load_row<HD>(dO, p.dout + (int64_t)ri * p.out_ld + h * HD);
-      float m = -INFINITY;
-      for (int j = 0; j < N; ++j) {
-        float acc = 0.f;
-#pragma unroll
-        for (int c = 0; c < H4; ++c) acc += dot4(q[c], KQ[j][c]);
-        acc += tab[rpb_index<WS>(i, j)];
-        if (g.shift > 0 && w.region(g, j) != reg_i) acc += -100.f;
-        Prow[j] = acc;
-        m = fmaxf(m, acc);
-      }
-      float l = 0.f;
-      for (int j = 0; j < N; ++j) {
-        const float e = __expf(Prow[j] - m);
-        Prow[j] = e;
-        l += e;
-      }
-      const float inv = 1.f / l;
       float D = 0.f;
-      for (int j = 0; j < N; ++j) {
-        const float pj = Prow[j] * inv;
-        Prow[j] = pj;
-        float dp = 0.f;
+      {
+        float4 o[H4];
+        load_row<HD>(o, p.out + (int64_t)ri * p.out_ld + h * HD);
 #pragma unroll
-        for (int c = 0; c < H4; ++c) dp += dot4(dO[c], VD[j][c]);
-        Srow[j] = dp;
-        D = fmaf(pj, dp, D);
+        for (int c = 0; c < H4; ++c) {
+          D += dot4(dO[c], o[c]);
+          q[c].x *= p.scale; q[c].y *= p.scale; q[c].z *= p.scale; q[c].w *= p.scale;
+        }
       }
+      const float lse = p.lse[rowbase + i];
       float4 dq[H4];
 #pragma unroll
       for (int c = 0; c < H4; ++c) dq[c] = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int j = 0; j < N; ++j) {
-        const float ds = Prow[j] * (Srow[j] - D);
-        Srow[j] = ds;
+        float s = 0.f, dp = 0.f;
+#pragma unroll
+        for (int c = 0; c < H4; ++c) { s += dot4(q[c], Ks[j][c]); dp += dot4(dO[c], Vs[j][c]); }
+        s += tab[rpb_index<WS>(i, j)];
+        if (g.shift > 0 && w.region(g, j) != reg_i) s += -100.f;
+        const float ds = __expf(s - lse) * (dp - D);
         atomicAdd(&tabg[rpb_index<WS>(i, j)], ds);
 #pragma unroll
         for (int c = 0; c < H4; ++c) {
-          const float4 kk = KQ[j][c];
+          const float4 kk = Ks[j][c];
           dq[c].x = fmaf(ds, kk.x, dq[c].x); dq[c].y = fmaf(ds, kk.y, dq[c].y);
           dq[c].z = fmaf(ds, kk.z, dq[c].z); dq[c].w = fmaf(ds, kk.w, dq[c].w);
         }
@@ -239,32 +226,69 @@ __global__ __launch_bounds__(64) void winattn_bwd_kernel(WinParams p) {
 #pragma unroll
       for (int c = 0; c < H4; ++c)
         dst[c] = make_float4(dq[c].x * p.scale, dq[c].y * p.scale, dq[c].z * p.scale, dq[c].w * p.scale);
+      p.dsum[rowbase + i] = D;
     } else {
-      // pad query: output cropped, so its P row contributes nothing downstream
-      for (int j = 0; j < N; ++j) { Prow[j] = 0.f; Srow[j] = 0.f; }
-#pragma unroll
-      for (int c = 0; c < H4; ++c) { q[c] = make_float4(0.f, 0.f, 0.f, 0.f); dO[c] = q[c]; }
+      p.dsum[rowbase + i] = 0.f;
     }
   }
   __syncthreads();
-  if (i < N) {
-#pragma unroll
-    for (int c = 0; c < H4; ++c) { KQ[i][c] = q[c]; VD[i][c] = dO[c]; }
-  }
-  __syncthreads();
+  float* P = p.partial + ((int64_t)win * g.heads + h) * (T + 2 * HD);
+  for (int e = lane; e < T; e += 64) P[e] = tabg[e];
+}
 
-  // ---------------- phase B: lane = key ----------------
+template <int WS, int HD>
+__global__ __launch_bounds__(64) void winattn_bwd_kv_kernel(WinParams p) {
+  constexpr int N = WS * WS, T = (2 * WS - 1) * (2 * WS - 1), H4 = HD / 4;
+  __shared__ float4 Qs[N][H4];  // scale * q
+  __shared__ float4 Ds[N][H4];  // dO
+  __shared__ float tab[T];
+  __shared__ float lse_s[N], D_s[N];
+  __shared__ int reg_s[N];
+  __shared__ float padk[HD], padv[HD];
+  const WinGeom& g = p.g;
+  const int win = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const Win<WS> w(g, win);
+  const int64_t rowbase = ((int64_t)win * g.heads + h) * N;
+  for (int e = lane; e < N * H4; e += 64) {
+    const int i = e / H4, q4 = e % H4;
+    const int r = w.row(g, i);
+    float4 qq = ld_tok4(p.q, p.qk_ld, r, p.q_pad, h * HD + 4 * q4);
+    qq.x *= p.scale; qq.y *= p.scale; qq.z *= p.scale; qq.w *= p.scale;
+    Qs[i][q4] = qq;
+    Ds[i][q4] = r >= 0 ? *reinterpret_cast<const float4*>(p.dout + (int64_t)r * p.out_ld + h * HD + 4 * q4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int e = lane; e < T; e += 64) tab[e] = p.rpb[e * g.heads + h];
+  if (lane < N) {
+    lse_s[lane] = p.lse[rowbase + lane];  // +inf for pad queries -> P = 0
+    D_s[lane] = p.dsum[rowbase + lane];
+    reg_s[lane] = g.shift > 0 ? w.region(g, lane) : 0;
+  }
+  if (lane < HD) { padk[lane] = 0.f; padv[lane] = 0.f; }
+  __syncthreads();
   const int j = lane;
   if (j < N) {
     const int rj = w.row(g, j);
-    float4 dk[H4], dv[H4];
+    const int reg_j = reg_s[j];
+    float4 kj[H4], vj[H4], dk[H4], dv[H4];
 #pragma unroll
-    for (int c = 0; c < H4; ++c) { dk[c] = make_float4(0.f, 0.f, 0.f, 0.f); dv[c] = dk[c]; }
-    for (int ii = 0; ii < N; ++ii) {
-      const float ds = dSs[ii * NP + j], pr = Ps[ii * NP + j];
+    for (int c = 0; c < H4; ++c) {
+      kj[c] = ld_tok4(p.k, p.qk_ld, rj, p.k_pad, h * HD + 4 * c);
+      vj[c] = ld_tok4(p.v, p.v_ld, rj, p.v_pad, h * HD + 4 * c);
+      dk[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      dv[c] = dk[c];
+    }
+    for (int i = 0; i < N; ++i) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int c = 0; c < H4; ++c) { s += dot4(Qs[i][c], kj[c]); dp += dot4(Ds[i][c], vj[c]); }
+      s += tab[rpb_index<WS>(i, j)];
+      if (g.shift > 0 && reg_s[i] != reg_j) s += -100.f;
+      const float pr = __expf(s - lse_s[i]);
+      const float ds = pr * (dp - D_s[i]);
 #pragma unroll
       for (int c = 0; c < H4; ++c) {
-        const float4 qq = KQ[ii][c], dd = VD[ii][c];
+        const float4 qq = Qs[i][c], dd = Ds[i][c];
         dk[c].x = fmaf(ds, qq.x, dk[c].x); dk[c].y = fmaf(ds, qq.y, dk[c].y);
         dk[c].z = fmaf(ds, qq.z, dk[c].z); dk[c].w = fmaf(ds, qq.w, dk[c].w);
         dv[c].x = fmaf(pr, dd.x, dv[c].x); dv[c].y = fmaf(pr, dd.y, dv[c].y);
@@ -288,7 +312,6 @@ __global__ __launch_bounds__(64) void winattn_bwd_kernel(WinParams p) {
   }
   __syncthreads();
   float* P = p.partial + ((int64_t)win * g.heads + h) * (T + 2 * HD);
-  for (int e = lane; e < T; e += 64) P[e] = tabg[e];
   if (lane < HD) { P[T + lane] = padk[lane]; P[T + HD + lane] = padv[lane]; }
 }
 
@@ -326,6 +349,7 @@ static int make_params(const mdemi_winattn_desc* d, WinParams& p, int& nwin) {
   p.v = d->v; p.v_ld = d->v_ld; p.v_pad = d->v_pad;
   p.rpb = d->rpb_table;
   p.out = d->out; p.out_ld = d->out_ld;
+  p.lse = d->lse;
   p.dout = d->dout; p.dq = d->dq; p.dk = d->dk; p.dqk_ld = d->dqk_ld; p.dv = d->dv; p.dv_ld = d->dv_ld;
   p.partial = (float*)d->workspace;
   nwin = d->B * p.g.nWh * p.g.nWw;
@@ -346,15 +370,16 @@ extern "C" int mdemi_winattn_fwd(const mdemi_winattn_desc* d, void* stream) {
   return check_launch("winattn_fwd");
 }
 
-// workspace: [partials nwin x heads*R | sums heads*R | colsum scratch]
+// workspace: [partials nwin x heads*R | D nwin x heads x N | sums heads*R | colsum scratch]
 static size_t wa_part_bytes(int nwin, int heads, int R) { return align_up((size_t)nwin * heads * R * 4, 256); }
+static size_t wa_dsum_bytes(int nwin, int heads, int N) { return align_up((size_t)nwin * heads * N * 4, 256); }
 extern "C" size_t mdemi_winattn_bwd_workspace_size(const mdemi_winattn_desc* d) {
   WinParams p;
   int nwin;
   if (make_params(d, p, nwin)) return 0;
   const int R = (2 * d->window - 1) * (2 * d->window - 1) + 2 * d->head_dim;
-  return wa_part_bytes(nwin, d->heads, R) + align_up((size_t)d->heads * R * 4, 256) +
-         colsum_ws_bytes(nwin, (int64_t)d->heads * R);
+  return wa_part_bytes(nwin, d->heads, R) + wa_dsum_bytes(nwin, d->heads, d->window * d->window) +
+         align_up((size_t)d->heads * R * 4, 256) + colsum_ws_bytes(nwin, (int64_t)d->heads * R);
 }
 
 extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
@@ -363,6 +388,7 @@ extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
   int rc = make_params(d, p, nwin);
   if (rc) return rc;
   MDEMI_REQUIRE(d->dout && d->dq && d->dk && d->dv && d->d_rpb_table, "winattn_bwd: null gradient buffer");
+  MDEMI_REQUIRE(d->out && d->lse, "winattn_bwd: needs the forward output and its saved lse");
   MDEMI_REQUIRE(d->dqk_ld % 4 == 0 && d->dv_ld % 4 == 0, "winattn_bwd: gradient strides must be %% 4");
   const size_t need = mdemi_winattn_bwd_workspace_size(d);
   if (!d->workspace || (size_t)d->workspace_bytes < need) {
@@ -370,9 +396,11 @@ extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
     return MDEMI_EWORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL((winattn_bwd_kernel<7, 32>), dim3(nwin, d->heads), dim3(64), 0, st, p);
   const int R = 13 * 13 + 64;
-  float* sums = (float*)((char*)d->workspace + wa_part_bytes(nwin, d->heads, R));
+  p.dsum = (float*)((char*)d->workspace + wa_part_bytes(nwin, d->heads, R));
+  hipLaunchKernelGGL((winattn_bwd_q_kernel<7, 32>), dim3(nwin, d->heads), dim3(64), 0, st, p);
+  hipLaunchKernelGGL((winattn_bwd_kv_kernel<7, 32>), dim3(nwin, d->heads), dim3(64), 0, st, p);
+  float* sums = (float*)((char*)p.dsum + wa_dsum_bytes(nwin, d->heads, 49));
   void* cws = (char*)sums + align_up((size_t)d->heads * R * 4, 256);
   int rc2 = colsum_launch(p.partial, nwin, (int64_t)d->heads * R, (int64_t)d->heads * R, sums, 0, cws, st);
   if (rc2) return rc2;

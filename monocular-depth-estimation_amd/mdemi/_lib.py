@@ -68,6 +68,7 @@ class WinAttnDesc(ctypes.Structure):
         ("v", vp), ("v_ld", i64), ("v_pad", vp),
         ("rpb_table", vp),
         ("out", vp), ("out_ld", i64),
+        ("lse", vp),
         ("dout", vp),
         ("dq", vp), ("dk", vp), ("dqk_ld", i64),
         ("dv", vp), ("dv_ld", i64),

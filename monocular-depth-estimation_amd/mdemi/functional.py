@@ -370,8 +370,12 @@ class _WindowAttnFn(torch.autograd.Function):
         d.v_pad = v_bias.data_ptr() + 4 * v_off if v_bias is not None else None
         d.rpb_table = rpb.data_ptr()
         d.out, d.out_ld = out.data_ptr(), C
+        ws = window
+        nwin = B * (-(-H // ws)) * (-(-W // ws))
+        lse = torch.empty(nwin, heads, ws * ws, device=qk.device, dtype=torch.float32)
+        d.lse = lse.data_ptr()
         L.check(L.load().mdemi_winattn_fwd(ctypes.byref(d), L.stream()), "winattn_fwd")
-        ctx.save_for_backward(qk, qk_bias, v, v_bias, rpb)
+        ctx.save_for_backward(qk, qk_bias, v, v_bias, rpb, out, lse)
         ctx.geom = geom
         ctx.has_qkb = qk_bias is not None
         ctx.has_vb = v_bias is not None
@@ -379,7 +383,7 @@ class _WindowAttnFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        qk, qk_bias, v, v_bias, rpb = ctx.saved_tensors
+        qk, qk_bias, v, v_bias, rpb, out, lse = ctx.saved_tensors
         B, H, W, heads, window, shift, scale, C, v_off = ctx.geom
         dout = _c(dout)
         dqk = torch.empty_like(qk)
@@ -403,7 +407,7 @@ class _WindowAttnFn(torch.autograd.Function):
         d.v, d.v_ld = v.data_ptr() + 4 * v_off, v.stride(0)
         d.v_pad = v_bias.data_ptr() + 4 * v_off if v_bias is not None else None
         d.rpb_table = rpb.data_ptr()
-        d.out_ld = C
+        d.out, d.out_ld, d.lse = out.data_ptr(), C, lse.data_ptr()
         d.dout = dout.data_ptr()
         d.dq, d.dk, d.dqk_ld = dqk.data_ptr(), dqk.data_ptr() + 4 * C, dqk.stride(0)
         d.dv, d.dv_ld = dv_t.data_ptr() + 4 * v_off, dv_t.stride(0)
