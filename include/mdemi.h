@@ -98,6 +98,9 @@ typedef struct mdemi_gemm_desc {
   int32_t split_k; int32_t _pad0;  /* >1: K split over workgroups, fp32 slabs in workspace */
   void* workspace; int64_t workspace_bytes;
   mdemi_conv_geom conv;            /* geometry for an MDEMI_L_CONV operand */
+  float* preact; int64_t ldpre; int64_t pre_bstride;  /* optional 2nd output: the value
+                                      before `act` (and before residual); lets fc1 store
+                                      both h and gelu(h) in one pass */
 } mdemi_gemm_desc;
 
 size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d);

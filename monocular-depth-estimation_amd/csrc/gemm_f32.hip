@@ -35,6 +35,16 @@ constexpr int GBM = 128, GBN = 128, GTHREADS = 256;
 constexpr int PMN = GBM + 4;   // [k][row] image pitch (floats)
 template <int BK> struct PitchK { static constexpr int v = BK + 4; };  // [row][k] image pitch
 
+struct FastDiv {
+  uint32_t mul, shift;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t c = 0;
+  while ((1u << c) < d) ++c;
+  const uint32_t L = 31 + c;
+  return FastDiv{(uint32_t)(((uint64_t)1 << L) / d + 1), L};
+}
+
 struct GemmParams {
   int M, N, K, batch, split, ktile_per_split;
   const float* A; int64_t lda, a_bs;
@@ -44,20 +54,38 @@ struct GemmParams {
   const float* bias; int bias_mode, act;
   const float* aux; int64_t ldaux, aux_bs;
   const float* res; int64_t ldres, res_bs;
+  float* pre; int64_t ldpre, pre_bs;  // optional pre-activation output
   float* slab;  // split-K partials [split][batch][M][N]
   mdemi_conv_geom cv;
+  FastDiv fd_c, fd_kw, fd_ow, fd_oh;  // conv index decomposition
   int a_vec, b_vec;  // 1: 16-byte vector loads legal for this operand
   int tiles_m, tiles_n, group_m;
 };
 
-__device__ __forceinline__ float4 ld4_guard(const float* p, int n_valid, bool vec) {
-  if (n_valid >= 4 && vec) return *reinterpret_cast<const float4*>(p);
-  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (n_valid > 0) r.x = p[0];
-  if (n_valid > 1) r.y = p[1];
-  if (n_valid > 2) r.z = p[2];
-  if (n_valid > 3) r.w = p[3];
-  return r;
+// ---------------------------------------------------------------------------
+// Branch-free operand fetch.  Dense operands use buffer loads through a
+// wave-uniform descriptor rebased to the current K tile (SALU work only);
+// out-of-range elements get the offset BUF_OOB, which the hardware range check
+// turns into zeros.  NHWC gathers use 64-bit loads from a clamped address and
+// zero the result with a select.  No per-element control flow in the K loop.
+// ---------------------------------------------------------------------------
+constexpr int BUF_OOB = (int)0x80000000u;
+constexpr int BUF_RECORDS = 0x7fffffff;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, BUF_RECORDS, 0x00020000);
+}
+__device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return *reinterpret_cast<float4*>(&v);
+}
+__device__ __forceinline__ float buf_ld1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// n / d for 0 <= n < 2^31 by multiply-shift (host-computed magic, exact).
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)(((uint64_t)(uint32_t)n * f.mul) >> f.shift);
 }
 
 template <int OP>
@@ -120,24 +148,34 @@ __device__ __forceinline__ void store_kr(float* lds, int t, const float4 (&r)[BK
 template <int LAYOUT, int OP, bool IS_A, int BK, bool TR>
 struct Loader;
 
-// dense [row][k]
+// dense [row][k]: thread t covers rows t/KQ + RS*q, k-quad t%KQ
 template <int OP, bool IS_A, int BK, bool TR>
 struct Loader<MDEMI_L_KCONTIG, OP, IS_A, BK, TR> {
   static constexpr int IMG = TR ? IMG_KT : IMG_RK, NQ = BK / 8, KQ = BK / 4, RS = 256 / KQ;
-  const float* base; int64_t ld; int rows, K; bool vec;
-  int row0; int kq;
-  __device__ void init(const float* p, int64_t ld_, int rows_, int K_, bool vec_, int r0, int t,
-                       const mdemi_conv_geom&) {
-    base = p; ld = ld_; rows = rows_; K = K_; vec = vec_;
-    row0 = r0 + t / KQ; kq = t % KQ;
+  const float* base; int K; bool vec;
+  int voff[NQ]; int kq;
+  __device__ void init(const float* p, int64_t ld, int rows, int K_, bool vec_, int r0, int t, const GemmParams&) {
+    base = p + (int64_t)r0 * ld; K = K_; vec = vec_; kq = t % KQ;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int row = t / KQ + RS * q;
+      voff[q] = r0 + row < rows ? (int)(((int64_t)row * ld + 4 * kq) * 4) : BUF_OOB;
+    }
   }
   __device__ void load(int k0, float4 (&r)[NQ]) const {
+    const auto rs = make_rsrc(base + k0);
     const int k = k0 + 4 * kq;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const int row = row0 + RS * q;
-      const int nv = (row < rows) ? min(4, K - k) : 0;
-      r[q] = apply_op<OP>(ld4_guard(base + (int64_t)row * ld + k, nv, vec));
+      if (vec) {
+        r[q] = buf_ld4(rs, k < K ? voff[q] : BUF_OOB);
+      } else {
+        r[q].x = buf_ld1(rs, k + 0 < K ? voff[q] + 0 : BUF_OOB);
+        r[q].y = buf_ld1(rs, k + 1 < K ? voff[q] + 4 : BUF_OOB);
+        r[q].z = buf_ld1(rs, k + 2 < K ? voff[q] + 8 : BUF_OOB);
+        r[q].w = buf_ld1(rs, k + 3 < K ? voff[q] + 12 : BUF_OOB);
+      }
+      r[q] = apply_op<OP>(r[q]);
     }
   }
   __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) {
@@ -145,45 +183,61 @@ struct Loader<MDEMI_L_KCONTIG, OP, IS_A, BK, TR> {
   }
 };
 
-// dense [k][row]
+// dense [k][row]: thread t covers k rows t/32 + 8q, column quad t%32
 template <int OP, bool IS_A, int BK, bool TR>
 struct Loader<MDEMI_L_MNCONTIG, OP, IS_A, BK, TR> {
   static constexpr int IMG = IMG_KR, NQ = BK / 8;
-  const float* base; int64_t ld; int rows, K; bool vec;
-  int col; int kl;
-  __device__ void init(const float* p, int64_t ld_, int rows_, int K_, bool vec_, int r0, int t,
-                       const mdemi_conv_geom&) {
-    base = p; ld = ld_; rows = rows_; K = K_; vec = vec_;
-    col = r0 + 4 * (t & 31); kl = t >> 5;
+  const float* base; int64_t ld; int K; bool vec;
+  int voff; int kl; int cvalid;  // valid columns of this thread's quad (0..4)
+  __device__ void init(const float* p, int64_t ld_, int cols, int K_, bool vec_, int c0, int t, const GemmParams&) {
+    base = p + c0; ld = ld_; K = K_; vec = vec_;
+    const int col = 4 * (t & 31);
+    kl = t >> 5;
+    cvalid = max(0, min(4, cols - c0 - col));
+    voff = (int)(((int64_t)kl * ld + col) * 4);
   }
   __device__ void load(int k0, float4 (&r)[NQ]) const {
+    const auto rs = make_rsrc(base + (int64_t)k0 * ld);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const int k = k0 + kl + 8 * q;
-      const int nv = (k < K) ? min(4, rows - col) : 0;
-      r[q] = apply_op<OP>(ld4_guard(base + (int64_t)k * ld + col, nv, vec));
+      const bool kin = k0 + kl + 8 * q < K;
+      const int off = voff + (int)(8 * q * ld * 4);
+      if (vec) {
+        r[q] = buf_ld4(rs, kin && cvalid > 0 ? off : BUF_OOB);
+      } else {
+        r[q].x = buf_ld1(rs, kin && cvalid > 0 ? off + 0 : BUF_OOB);
+        r[q].y = buf_ld1(rs, kin && cvalid > 1 ? off + 4 : BUF_OOB);
+        r[q].z = buf_ld1(rs, kin && cvalid > 2 ? off + 8 : BUF_OOB);
+        r[q].w = buf_ld1(rs, kin && cvalid > 3 ? off + 12 : BUF_OOB);
+      }
+      r[q] = apply_op<OP>(r[q]);
     }
   }
   __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) { store_kr<BK>(lds, t, r); }
 };
+
+__device__ __forceinline__ float4 gather4(const float* base, int64_t idx, bool ok) {
+  const float4 v = *reinterpret_cast<const float4*>(base + (ok ? idx : 0));
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
 
 // Implicit im2col of an NHWC activation, operand A (row = output pixel,
 // k = (ky,kx,c)).  Requires C % 4 == 0 so a k-quad never straddles a tap.
 template <int OP, int BK, bool TR>
 struct Loader<MDEMI_L_CONV, OP, true, BK, TR> {
   static constexpr int IMG = TR ? IMG_KT : IMG_RK, NQ = BK / 8, KQ = BK / 4, RS = 256 / KQ;
-  const float* base; mdemi_conv_geom g; int rows, K; int kq;
+  const float* base; mdemi_conv_geom g; FastDiv fc, fkw; int K; int kq;
   int n[NQ], iy0[NQ], ix0[NQ]; bool valid[NQ];
-  __device__ void init(const float* p, int64_t, int rows_, int K_, bool, int r0, int t, const mdemi_conv_geom& g_) {
-    base = p; g = g_; rows = rows_; K = K_; kq = t % KQ;
+  __device__ void init(const float* p, int64_t, int rows, int K_, bool, int r0, int t, const GemmParams& P) {
+    base = p; g = P.cv; fc = P.fd_c; fkw = P.fd_kw; K = K_; kq = t % KQ;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int i = r0 + t / KQ + RS * q;
       valid[q] = i < rows;
       const int ii = valid[q] ? i : 0;
-      const int ox = ii % g.ow, tmp = ii / g.ow;
-      const int oy = tmp % g.oh;
-      n[q] = tmp / g.oh;
+      const int tmp = fdiv(ii, P.fd_ow), ox = ii - tmp * g.ow;
+      const int nn = fdiv(tmp, P.fd_oh), oy = tmp - nn * g.oh;
+      n[q] = nn;
       iy0[q] = oy * g.stride - g.pad;
       ix0[q] = ox * g.stride - g.pad;
     }
@@ -192,8 +246,8 @@ struct Loader<MDEMI_L_CONV, OP, true, BK, TR> {
     const int k = k0 + 4 * kq;
     const bool kin = k < K;
     const int kk = kin ? k : 0;
-    const int c = kk % g.c, tap = kk / g.c;
-    const int kx = tap % g.kw, ky = tap / g.kw;
+    const int tap = fdiv(kk, fc), c = kk - tap * g.c;
+    const int ky = fdiv(tap, fkw), kx = tap - ky * g.kw;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       int iy = iy0[q] + ky, ix = ix0[q] + kx;
@@ -203,9 +257,7 @@ struct Loader<MDEMI_L_CONV, OP, true, BK, TR> {
       } else {
         ok = ok && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
       }
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) v = *reinterpret_cast<const float4*>(base + (((int64_t)n[q] * g.h + iy) * g.w + ix) * g.c + c);
-      r[q] = apply_op<OP>(v);
+      r[q] = apply_op<OP>(gather4(base, (((int64_t)n[q] * g.h + iy) * g.w + ix) * g.c + c, ok));
     }
   }
   __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) {
@@ -218,14 +270,17 @@ struct Loader<MDEMI_L_CONV, OP, true, BK, TR> {
 template <int OP, int BK, bool TR>
 struct Loader<MDEMI_L_CONV, OP, false, BK, TR> {
   static constexpr int IMG = IMG_KR, NQ = BK / 8;
-  const float* base; mdemi_conv_geom g; int cols, K; int kl;
+  const float* base; mdemi_conv_geom g; FastDiv fow, foh; int K; int kl;
   int c, ky, kx; bool jvalid;
-  __device__ void init(const float* p, int64_t, int cols_, int K_, bool, int c0, int t, const mdemi_conv_geom& g_) {
-    base = p; g = g_; cols = cols_; K = K_; kl = t >> 5;
+  __device__ void init(const float* p, int64_t, int cols, int K_, bool, int c0, int t, const GemmParams& P) {
+    base = p; g = P.cv; fow = P.fd_ow; foh = P.fd_oh; K = K_; kl = t >> 5;
     const int j = c0 + 4 * (t & 31);
     jvalid = j < cols;
     const int jj = jvalid ? j : 0;
-    c = jj % g.c; const int tap = jj / g.c; kx = tap % g.kw; ky = tap / g.kw;
+    const int tap = fdiv(jj, P.fd_c);
+    c = jj - tap * g.c;
+    ky = fdiv(tap, P.fd_kw);
+    kx = tap - ky * g.kw;
   }
   __device__ void load(int k0, float4 (&r)[NQ]) const {
 #pragma unroll
@@ -233,27 +288,27 @@ struct Loader<MDEMI_L_CONV, OP, false, BK, TR> {
       const int k = k0 + kl + 8 * q;
       bool ok = jvalid && k < K;
       const int kk = ok ? k : 0;
-      const int ox = kk % g.ow, tmp = kk / g.ow;
-      const int oy = tmp % g.oh, nn = tmp / g.oh;
+      const int tmp = fdiv(kk, fow), ox = kk - tmp * g.ow;
+      const int nn = fdiv(tmp, foh), oy = tmp - nn * g.oh;
       int iy = oy * g.stride - g.pad + ky, ix = ox * g.stride - g.pad + kx;
       if (g.pad_mode == MDEMI_PAD_REPLICATE) {
         iy = min(max(iy, 0), g.h - 1); ix = min(max(ix, 0), g.w - 1);
       } else {
         ok = ok && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
       }
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) v = *reinterpret_cast<const float4*>(base + (((int64_t)nn * g.h + iy) * g.w + ix) * g.c + c);
-      r[q] = apply_op<OP>(v);
+      r[q] = apply_op<OP>(gather4(base, (((int64_t)nn * g.h + iy) * g.w + ix) * g.c + c, ok));
     }
   }
   __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) { store_kr<BK>(lds, t, r); }
 };
+
 
 __device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int i, int j, float acc) {
   float v = p.alpha * acc;
   if (p.beta != 0.f) v += p.beta * p.C[(int64_t)b * p.c_bs + (int64_t)i * p.ldc + j];
   if (p.bias_mode == MDEMI_BIAS_COL) v += p.bias[j];
   else if (p.bias_mode == MDEMI_BIAS_ROW) v += p.bias[i];
+  if (p.pre) p.pre[(int64_t)b * p.pre_bs + (int64_t)i * p.ldpre + j] = v;
   if (p.act == MDEMI_ACT_GELU_GRAD) v *= gelu_grad_f(p.aux[(int64_t)b * p.aux_bs + (int64_t)i * p.ldaux + j]);
   else if (p.act != MDEMI_ACT_NONE) v = apply_act(p.act, v);
   if (p.res) v += p.res[(int64_t)b * p.res_bs + (int64_t)i * p.ldres + j];
@@ -305,8 +360,8 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(GemmParams p) {
 
   LA la;
   LB lb;
-  la.init(p.A + (int64_t)b * p.a_bs, p.lda, p.M, p.K, p.a_vec, bm, t, p.cv);
-  lb.init(p.B + (int64_t)b * p.b_bs, p.ldb, p.N, p.K, p.b_vec, bn, t, p.cv);
+  la.init(p.A + (int64_t)b * p.a_bs, p.lda, p.M, p.K, p.a_vec, bm, t, p);
+  lb.init(p.B + (int64_t)b * p.b_bs, p.ldb, p.N, p.K, p.b_vec, bn, t, p);
 
   const int ktiles_total = (p.K + BK - 1) / BK;
   const int kt_begin = sidx * p.ktile_per_split;
@@ -376,37 +431,95 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(GemmParams p) {
     }
   }
 
-  // Epilogue.  acc[tm][tn][r] holds C(row, col) with
-  //   row = bm + wm*64 + tm*32 + (r&3) + 8*(r>>2) + 4*h,  col = bn + wn*64 + tn*32 + l31
+  // Epilogue.  acc[im][in][r] holds C(row, col) with
+  //   row = bm + wm*64 + im*32 + (r&3) + 8*(r>>2) + 4*h,  col = bn + wn*64 + in*32 + l31
+  // Every operand is addressed through a buffer descriptor at the tile origin
+  // with 32-bit offsets; out-of-tile elements get BUF_OOB (loads read 0,
+  // stores are dropped), so the fused stages below are straight-line code
+  // with wave-uniform stage selection.
+  int colb[2];
+  bool colok[2];
+#pragma unroll
+  for (int in = 0; in < 2; ++in) {
+    const int jl = wn * 64 + in * 32 + l31;
+    colok[in] = bn + jl < p.N;
+    colb[in] = jl;
+  }
+  auto rowl = [&](int im, int r) { return wm * 64 + im * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
+  auto off = [&](int64_t ld, int im, int in, int r) {
+    const int il = rowl(im, r);
+    return (colok[in] && bm + il < p.M) ? (int)((il * ld + colb[in]) * 4) : BUF_OOB;
+  };
+#define MDEMI_EACH for (int r = 0; r < 16; ++r)
   if (p.split > 1) {
-    float* S = p.slab + ((int64_t)sidx * p.batch + b) * (int64_t)p.M * p.N;
+    const auto rs = make_rsrc(p.slab + (((int64_t)sidx * p.batch + b) * p.M + bm) * p.N + bn);
 #pragma unroll
     for (int im = 0; im < 2; ++im)
 #pragma unroll
-      for (int in = 0; in < 2; ++in) {
-        const int j = bn + wn * 64 + in * 32 + l31;
-        if (j >= p.N) continue;
+      for (int in = 0; in < 2; ++in)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = bm + wm * 64 + im * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (i < p.M) S[(int64_t)i * p.N + j] = acc[im][in][r];
-        }
-      }
+        MDEMI_EACH __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[im][in][r]), rs, off(p.N, im, in, r), 0, 0);
     return;
   }
-  float* Cb = p.C + (int64_t)b * p.c_bs;
+  const int64_t cbase = (int64_t)b * p.c_bs + (int64_t)bm * p.ldc + bn;
+  const auto rc = make_rsrc(p.C + cbase);
+  // one 32x32 accumulator at a time keeps the epilogue's live offsets to 16
 #pragma unroll
   for (int im = 0; im < 2; ++im)
 #pragma unroll
     for (int in = 0; in < 2; ++in) {
-      const int j = bn + wn * 64 + in * 32 + l31;
-      if (j >= p.N) continue;
+      floatx16& v = acc[im][in];
+      if (p.alpha != 1.f) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = bm + wm * 64 + im * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (i < p.M) Cb[(int64_t)i * p.ldc + j] = epilogue_value(p, b, i, j, acc[im][in][r]);
+        MDEMI_EACH v[r] *= p.alpha;
       }
+      if (p.beta != 0.f) {
+#pragma unroll
+        MDEMI_EACH v[r] = fmaf(p.beta, buf_ld1(rc, off(p.ldc, im, in, r)), v[r]);
+      }
+      if (p.bias_mode == MDEMI_BIAS_COL) {
+        const float bj = colok[in] ? p.bias[bn + colb[in]] : 0.f;
+#pragma unroll
+        MDEMI_EACH v[r] += bj;
+      } else if (p.bias_mode == MDEMI_BIAS_ROW) {
+        const auto rs = make_rsrc(p.bias + bm);
+#pragma unroll
+        MDEMI_EACH v[r] += buf_ld1(rs, bm + rowl(im, r) < p.M ? rowl(im, r) * 4 : BUF_OOB);
+      }
+      if (p.pre) {
+        const auto rs = make_rsrc(p.pre + (int64_t)b * p.pre_bs + (int64_t)bm * p.ldpre + bn);
+#pragma unroll
+        MDEMI_EACH __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rs, off(p.ldpre, im, in, r), 0, 0);
+      }
+      switch (p.act) {
+        case MDEMI_ACT_GELU: {
+#pragma unroll
+          MDEMI_EACH v[r] = gelu_f(v[r]);
+        } break;
+        case MDEMI_ACT_RELU: {
+#pragma unroll
+          MDEMI_EACH v[r] = fmaxf(v[r], 0.f);
+        } break;
+        case MDEMI_ACT_GELU_GRAD: {
+          const auto rs = make_rsrc(p.aux + (int64_t)b * p.aux_bs + (int64_t)bm * p.ldaux + bn);
+#pragma unroll
+          MDEMI_EACH v[r] *= gelu_grad_f(buf_ld1(rs, off(p.ldaux, im, in, r)));
+        } break;
+        case MDEMI_ACT_NONE: break;
+        default: {
+#pragma unroll
+          MDEMI_EACH v[r] = apply_act(p.act, v[r]);
+        }
+      }
+      if (p.res) {
+        const auto rs = make_rsrc(p.res + (int64_t)b * p.res_bs + (int64_t)bm * p.ldres + bn);
+#pragma unroll
+        MDEMI_EACH v[r] += buf_ld1(rs, off(p.ldres, im, in, r));
+      }
+#pragma unroll
+      MDEMI_EACH __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rc, off(p.ldc, im, in, r), 0, 0);
     }
+#undef MDEMI_EACH
 }
 
 // Deterministic split-K combine + epilogue: sums slabs in split order.
@@ -497,6 +610,12 @@ static int validate(const mdemi_gemm_desc* d) {
     MDEMI_REQUIRE(al16(d->a_layout == MDEMI_L_CONV ? d->A : d->B), "gemm: conv operand must be 16-B aligned");
   }
   MDEMI_REQUIRE(d->bias_mode == MDEMI_BIAS_NONE || d->bias, "gemm: bias pointer missing");
+  // tile-relative 32-bit buffer offsets: 128 rows (or 16 k-rows) of any leading dimension
+  const int64_t lim = (int64_t)1 << 21;
+  MDEMI_REQUIRE(d->lda < lim && d->ldb < lim && d->ldc < lim && d->ldaux < lim && d->ldres < lim &&
+                    d->ldpre < lim, "gemm: leading dimension too large for 32-bit tile offsets");
+  if (d->split_k > 1)
+    MDEMI_REQUIRE(d->N < lim, "gemm: N too large for split-K slabs");
   MDEMI_REQUIRE(d->act != MDEMI_ACT_GELU_GRAD || d->aux, "gemm: GELU-grad epilogue needs aux");
   return MDEMI_OK;
 }
@@ -512,13 +631,22 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p) {
   p.aux = d->aux; p.ldaux = d->ldaux; p.aux_bs = d->aux_bstride;
   p.res = d->residual; p.ldres = d->ldres; p.res_bs = d->res_bstride;
   p.cv = d->conv;
+  p.pre = d->preact; p.ldpre = d->ldpre; p.pre_bs = d->pre_bstride;
   const int ktiles = (int)cdiv(d->K, GBK);
   int split = d->split_k < ktiles ? d->split_k : ktiles;
   p.ktile_per_split = (int)cdiv(ktiles, split);
   p.split = (int)cdiv(ktiles, p.ktile_per_split);
-  // vector loads need every row start 16-B aligned
-  p.a_vec = al16(d->A) && (d->lda % 4 == 0) && (d->a_bstride % 4 == 0);
-  p.b_vec = al16(d->B) && (d->ldb % 4 == 0) && (d->b_bstride % 4 == 0);
+  // vector loads need every row start 16-B aligned and whole quads in range
+  // (KCONTIG: K % 4; MNCONTIG: the row/column extent % 4)
+  p.a_vec = al16(d->A) && (d->lda % 4 == 0) && (d->a_bstride % 4 == 0) &&
+            (d->a_layout == MDEMI_L_KCONTIG ? d->K % 4 == 0 : d->M % 4 == 0);
+  p.b_vec = al16(d->B) && (d->ldb % 4 == 0) && (d->b_bstride % 4 == 0) &&
+            (d->b_layout == MDEMI_L_KCONTIG ? d->K % 4 == 0 : d->N % 4 == 0);
+  if (d->a_layout == MDEMI_L_CONV || d->b_layout == MDEMI_L_CONV) {
+    const mdemi_conv_geom& g = d->conv;
+    p.fd_c = make_fastdiv(g.c); p.fd_kw = make_fastdiv(g.kw);
+    p.fd_ow = make_fastdiv(g.ow); p.fd_oh = make_fastdiv(g.oh);
+  }
   p.slab = nullptr;
   p.tiles_m = (int)cdiv(d->M, GBM);
   p.tiles_n = (int)cdiv(d->N, GBN);

@@ -55,6 +55,7 @@ class GemmDesc(ctypes.Structure):
         ("split_k", i32), ("_pad0", i32),
         ("workspace", vp), ("workspace_bytes", i64),
         ("conv", ConvGeom),
+        ("preact", vp), ("ldpre", i64), ("pre_bstride", i64),
     ]
 
 

@@ -48,7 +48,7 @@ def _split_for(M, N, K):
 def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE, b_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
-         res_bstride=0, split_k=None, conv=None):
+         res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0):
     d = L.GemmDesc()
     d.M, d.N, d.K, d.batch = M, N, K, batch
     d.A, d.lda, d.a_bstride, d.a_layout, d.a_op = A.data_ptr(), lda, a_bstride, a_layout, a_op
@@ -61,6 +61,8 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     d.split_k = split_k if split_k is not None else _split_for(M, N, K)
     if conv is not None:
         d.conv = conv
+    if preact is not None:
+        d.preact, d.ldpre, d.pre_bstride = preact.data_ptr(), ldpre, pre_bstride
     lib = L.load()
     need = lib.mdemi_gemm_workspace_size(ctypes.byref(d))
     if need:
@@ -141,6 +143,65 @@ class _LinearFn(torch.autograd.Function):
 def linear(x, weight, bias=None, residual=None, in_gelu=False):
     """y = (gelu(x) if in_gelu else x) @ W^T + b (+ residual)."""
     return _LinearFn.apply(x, weight, bias, residual, in_gelu)
+
+
+class _MlpFn(torch.autograd.Function):
+    """fc1 -> GELU -> fc2 (+ residual), Swin/NeW-CRF Mlp (swin_transformer.py:11-29).
+
+    fc1's epilogue writes both h (pre-activation) and g = gelu(h): HBM is
+    plentiful and one extra [rows, 4C] store is far cheaper than recomputing
+    gelu in fc2's operand loader for every N-tile.  Backward: fc2's dgrad
+    epilogue multiplies by gelu'(h) (reading h), so dh never exists unfused."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, residual):
+        _require_cuda(x, w1, b1, w2, b2, residual)
+        K = x.shape[-1]
+        x2 = _c(x).reshape(-1, K)
+        M = x2.shape[0]
+        Hd, N = w1.shape[0], w2.shape[0]
+        h = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
+        g = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
+        gemm(x2, _c(w1), g, M, Hd, K, lda=K, ldb=K, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+             bias=b1, bias_mode=L.BIAS_COL if b1 is not None else L.BIAS_NONE, act=L.ACT_GELU,
+             preact=h, ldpre=Hd, split_k=1)
+        res2 = _c(residual).reshape(M, N) if residual is not None else None
+        out = linear_fwd_raw(g, _c(w2), b2, residual=res2)
+        ctx.save_for_backward(x2, w1, w2, h, g)
+        ctx.flags = (b1 is not None, b2 is not None, residual is not None)
+        ctx.xshape = x.shape
+        return out.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, w2, h, g = ctx.saved_tensors
+        has_b1, has_b2, has_res = ctx.flags
+        M, K = x2.shape
+        Hd, N = w1.shape[0], w2.shape[0]
+        dy2 = _c(dy).reshape(M, N)
+        dev = dy.device
+        dw2 = torch.empty(N, Hd, device=dev, dtype=torch.float32)
+        gemm(dy2, g, dw2, N, Hd, M, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG)
+        db2 = colsum(dy2) if has_b2 else None
+        dh = torch.empty(M, Hd, device=dev, dtype=torch.float32)
+        gemm(dy2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
+             act=L.ACT_GELU_GRAD, aux=h, ldaux=Hd)
+        del h, g
+        dw1 = torch.empty(Hd, K, device=dev, dtype=torch.float32)
+        gemm(dh, x2, dw1, Hd, K, M, lda=Hd, ldb=K, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG)
+        db1 = colsum(dh) if has_b1 else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, device=dev, dtype=torch.float32)
+            gemm(dh, w1, dx, M, K, Hd, lda=Hd, ldb=K, ldc=K, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
+            dx = dx.view(ctx.xshape)
+        dres = dy if has_res and ctx.needs_input_grad[5] else None
+        return dx, dw1, db1, dw2, db2, dres
+
+
+def mlp(x, w1, b1, w2, b2, residual=None):
+    """fc2(gelu(fc1(x))) (+ residual) with nn.GELU (exact erf)."""
+    return _MlpFn.apply(x, w1, b1, w2, b2, residual)
 
 
 # --------------------------------------------------------------------------

@@ -29,8 +29,8 @@ def relative_position_index(ws):  # swin_transformer.py:91-101
 
 
 class Mlp(nn.Module):
-    """fc1 -> GELU -> fc2 (swin_transformer.py:11-29).  GELU is applied by fc2's
-    operand loader, so the 4C-wide activation is never written to HBM."""
+    """fc1 -> GELU -> fc2 (swin_transformer.py:11-29), one fused autograd op
+    (functional.mlp: fc1's epilogue applies GELU and also keeps h for gelu')."""
 
     def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.0):
         super().__init__()
@@ -44,8 +44,7 @@ class Mlp(nn.Module):
             raise ValueError("Mlp: only the reference's nn.GELU activation is built")
 
     def forward(self, x, residual=None):
-        h = mf.linear(x, self.fc1.weight, self.fc1.bias)
-        return mf.linear(h, self.fc2.weight, self.fc2.bias, residual=residual, in_gelu=True)
+        return mf.mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual=residual)
 
 
 class WindowAttention(nn.Module):

@@ -67,6 +67,23 @@ def test_linear_gelu_on_load(mf):
     close(wg.grad, wr.grad, rtol=1e-4)
 
 
+@pytest.mark.parametrize("M,C", [(333, 24), (4100, 96)])
+def test_mlp_fused(mf, M, C):
+    """fc1 -> GELU -> fc2 + residual with fc1 writing both h and gelu(h)."""
+    x, w1, b1 = rnd(M, C, seed=20), rnd(4 * C, C, seed=21, scale=0.3), rnd(4 * C, seed=22)
+    w2, b2, res = rnd(C, 4 * C, seed=23, scale=0.2), rnd(C, seed=24), rnd(M, C, seed=25)
+    dy = rnd(M, C, seed=26)
+    ref = [t.clone().requires_grad_() for t in (x, w1, b1, w2, b2, res)]
+    yr = F.linear(F.gelu(F.linear(ref[0], ref[1], ref[2])), ref[3], ref[4]) + ref[5]
+    yr.backward(dy)
+    gpu = [t.float().to(DEV).requires_grad_() for t in (x, w1, b1, w2, b2, res)]
+    yg = mf.mlp(*gpu)
+    yg.backward(dy.float().to(DEV))
+    close(yg, yr, rtol=1e-4)
+    for a, b in zip(gpu, ref):
+        close(a.grad, b.grad, rtol=1e-4 * max(1, math.sqrt(M / 300)))
+
+
 def test_gemm_splitk_and_batch(mf):
     from mdemi import _lib as L
     B, M, N, K = 3, 70, 90, 1000
