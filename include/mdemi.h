@@ -105,8 +105,10 @@ typedef struct mdemi_gemm_desc {
 
 size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d);
 int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream);
-/* tuning hook: pipelining variant (0..4, see gemm_f32.hip) and tile raster
- * (group_m > 0: XCD-aware grouped raster, 0: plain).  Process-global. */
+/* tuning hook: pipelining variant (0..5, see gemm_f32.hip; -1 = time the
+ * candidates once per distinct shape and cache the winner, the default -- all
+ * variants produce bit-identical results) and tile raster (group_m > 0:
+ * XCD-aware grouped raster, 0: plain).  Process-global. */
 int mdemi_gemm_set_variant(int32_t variant, int32_t group_m);
 
 /* column / row sums (bias gradients: db[j] = sum_i dY[i][j])

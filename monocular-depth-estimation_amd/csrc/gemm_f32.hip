@@ -27,6 +27,10 @@
 // and B column-panels in that XCD's L2 (guide T1).  Variants: see pick_variant.
 #include "common.h"
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 namespace mdemi {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -340,8 +344,8 @@ __device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles
 //   BK    K depth per LDS tile (16 or 32)
 //   NBUF  LDS buffers (2: write the next tile while others read this one)
 //   PREF  register prefetch of the next tile before the MFMAs (issue early / write late)
-template <int AL, int BL, int AOP, int BOP, int BK, int NBUF, bool PREF, bool TR>
-__global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(GemmParams p) {
+template <int AL, int BL, int AOP, int BOP, int BK, int NBUF, bool PREF, bool TR, int OCC>
+__global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void gemm_f32_kernel(GemmParams p) {
   using LA = Loader<AL, AOP, true, BK, TR>;
   using LB = Loader<BL, BOP, false, BK, TR>;
   constexpr int FA = Img<LA::IMG, BK>::floats, FB = Img<LB::IMG, BK>::floats;
@@ -539,22 +543,32 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
 
 using KernelFn = void (*)(GemmParams);
 
-// Variant table (benchmark hook mdemi_gemm_set_variant).  Measured on the
-// NewCRFs-L07 480x640 bs=8 shapes (tools/gemm_bench.py, profiles/r01_gemm_variants.log):
-//   BK16/NBUF2/prefetch with k-contiguous operands TRANSPOSED into [k][row]
-//   images (ds_read_b32 fragments) 80 TF; the same with [row][k] images and
-//   ds_read_b128 fragments 69 TF; BK32 (2 LDS buffers) 58 TF (VGPRs 170 ->
-//   2 waves/SIMD); BK32 single buffer 64-73 TF; plain load/barrier/compute
-//   BK16 75-79 TF.  XCD-grouped raster vs plain: +0.5 TF.
-//   0 (default): BK16 NBUF2 PREF transposed     1: BK16 NBUF2 PREF [row][k]
-static int g_variant = 0;
+// Variants (tools/gemm_bench.py on the NewCRFs-L07 480x640 bs=8 shapes,
+// profiles/r01_gemm_variants_v2.log):
+//   0: BK16, 2 LDS buffers, register prefetch, k-contiguous operands transposed
+//      into [k][row] images (ds_read_b32 fragments)
+//   1: as 0 with [row][k] images (ds_read_b128 fragments)
+//   2: as 0 capped at 128 VGPRs (4 waves/SIMD; spills)
+//   3: BK32, 2 buffers (2 workgroups/CU by LDS)   4: BK32, 1 buffer   5: as 3, [row][k]
+// No variant wins every shape (e.g. weight-gradient GEMMs over few output
+// tiles want BK32/2 buffers, token-major forwards want BK32/1 buffer), so by
+// default each distinct (layouts, ops, M, N, K, batch, split) is timed once
+// over the candidates on first use and the winner cached.  All variants add
+// the k products in the same order and split K at the same 32-element
+// boundaries, so the choice never changes a result bit.
+constexpr int NVARIANTS = 6;
+static int g_variant = -1;  // -1: autotune per shape
 static int g_group_m = 8;
 
 template <int AL, int BL, int AOP, int BOP>
 static KernelFn pick_variant(int v) {
   switch (v) {
-    case 1: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, false>;
-    default: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true>;
+    case 1: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, false, 2>;
+    case 2: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 4>;
+    case 3: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, true, 2>;
+    case 4: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 1, true, true, 2>;
+    case 5: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, false, 2>;
+    default: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 2>;
   }
 }
 
@@ -585,7 +599,7 @@ static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
   return nullptr;
 }
 
-static int variant_bk(int) { return 16; }
+static int variant_bk(int v) { return v >= 3 ? 32 : 16; }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -620,8 +634,8 @@ static int validate(const mdemi_gemm_desc* d) {
   return MDEMI_OK;
 }
 
-static void fill_params(const mdemi_gemm_desc* d, GemmParams& p) {
-  const int GBK = variant_bk(g_variant);
+static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant) {
+  const int GBK = variant_bk(variant);
   p.M = d->M; p.N = d->N; p.K = d->K; p.batch = d->batch;
   p.A = d->A; p.lda = d->lda; p.a_bs = d->a_bstride;
   p.B = d->B; p.ldb = d->ldb; p.b_bs = d->b_bstride;
@@ -632,10 +646,12 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p) {
   p.res = d->residual; p.ldres = d->ldres; p.res_bs = d->res_bstride;
   p.cv = d->conv;
   p.pre = d->preact; p.ldpre = d->ldpre; p.pre_bs = d->pre_bstride;
-  const int ktiles = (int)cdiv(d->K, GBK);
-  int split = d->split_k < ktiles ? d->split_k : ktiles;
-  p.ktile_per_split = (int)cdiv(ktiles, split);
-  p.split = (int)cdiv(ktiles, p.ktile_per_split);
+  // split boundaries in 32-element K chunks whatever the variant's BK
+  const int kc = (int)cdiv(d->K, 32);
+  const int split = d->split_k < kc ? d->split_k : kc;
+  const int chunks_per_split = (int)cdiv(kc, split);
+  p.ktile_per_split = chunks_per_split * (32 / GBK);
+  p.split = (int)cdiv(kc, chunks_per_split);
   // vector loads need every row start 16-B aligned and whole quads in range
   // (KCONTIG: K % 4; MNCONTIG: the row/column extent % 4)
   p.a_vec = al16(d->A) && (d->lda % 4 == 0) && (d->a_bstride % 4 == 0) &&
@@ -657,25 +673,15 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p) {
 
 using namespace mdemi;
 
-extern "C" size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d) {
-  if (!d || d->split_k <= 1) return 0;
-  GemmParams p;
-  fill_params(d, p);
-  if (p.split <= 1) return 0;
-  return (size_t)p.split * d->batch * (size_t)d->M * d->N * sizeof(float);
-}
-
-extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {
-  int rc = validate(d);
-  if (rc) return rc;
-  KernelFn fn = pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, g_variant);
+static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
+  KernelFn fn = pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant);
   if (!fn) {
     set_error("gemm: unsupported layout/op combination a=%d/%d b=%d/%d", d->a_layout, d->a_op, d->b_layout,
               d->b_op);
     return MDEMI_EUNSUP;
   }
   GemmParams p;
-  fill_params(d, p);
+  fill_params(d, p, variant);
   if (p.split > 1) {
     const size_t need = (size_t)p.split * d->batch * (size_t)d->M * d->N * sizeof(float);
     if (!d->workspace || (size_t)d->workspace_bytes < need) {
@@ -684,7 +690,6 @@ extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {
     }
     p.slab = (float*)d->workspace;
   }
-  hipStream_t st = (hipStream_t)stream;
   const int64_t nblocks = (int64_t)p.tiles_m * p.tiles_n * d->batch * p.split;
   MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
   hipLaunchKernelGGL(fn, dim3((unsigned)nblocks), dim3(GTHREADS), 0, st, p);
@@ -696,10 +701,76 @@ extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {
   return check_launch("gemm_f32");
 }
 
-// Benchmark/tuning hook: select the pipelining variant (see pick_variant) and
-// the tile raster (group_m > 0: XCD-aware grouped raster; 0: plain).
+struct TuneKey {
+  int al, bl, aop, bop, M, N, K, batch, split;
+  bool operator<(const TuneKey& o) const {
+    return std::tie(al, bl, aop, bop, M, N, K, batch, split) <
+           std::tie(o.al, o.bl, o.aop, o.bop, o.M, o.N, o.K, o.batch, o.split);
+  }
+};
+static std::map<TuneKey, int> g_tuned;
+static std::mutex g_tune_mu;
+
+// Re-running the GEMM is only harmless when C is write-only and aliases no input.
+static bool tunable(const mdemi_gemm_desc* d, hipStream_t st) {
+  if (d->beta != 0.f) return false;
+  const void* c = d->C;
+  if (c == d->A || c == d->B || c == d->residual || c == d->aux || c == d->bias) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  return true;
+}
+
+static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st) {
+  if (g_variant >= 0) return g_variant;
+  const TuneKey key{d->a_layout, d->b_layout, d->a_op, d->b_op, d->M, d->N, d->K, d->batch, d->split_k};
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    auto it = g_tuned.find(key);
+    if (it != g_tuned.end()) return it->second;
+  }
+  if (!tunable(d, st)) return 0;
+  static const int cands[] = {0, 1, 3, 4, 5};
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 0;
+  int best = 0;
+  float best_ms = 1e30f;
+  for (int v : cands) {
+    if (launch(d, v, st) != MDEMI_OK) continue;  // warm (and validate)
+    (void)hipEventRecord(e0, st);
+    for (int r = 0; r < 3; ++r) launch(d, v, st);
+    (void)hipEventRecord(e1, st);
+    float ms = 0.f;
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+    if (ms < best_ms) { best_ms = ms; best = v; }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tuned[key] = best;
+  return best;
+}
+
+extern "C" size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d) {
+  if (!d || d->split_k <= 1) return 0;
+  GemmParams p;
+  fill_params(d, p, 0);  // the split count does not depend on the variant
+  if (p.split <= 1) return 0;
+  return (size_t)p.split * d->batch * (size_t)d->M * d->N * sizeof(float);
+}
+
+extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {
+  int rc = validate(d);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  return launch(d, choose_variant(d, st), st);
+}
+
+// Benchmark/tuning hook: force a pipelining variant (see pick_variant; -1 =
+// per-shape autotune, the default) and the tile raster (group_m > 0:
+// XCD-aware grouped raster; 0: plain).
 extern "C" int mdemi_gemm_set_variant(int32_t variant, int32_t group_m) {
-  MDEMI_REQUIRE(variant >= 0 && variant <= 1 && group_m >= 0, "gemm_set_variant: bad args");
+  MDEMI_REQUIRE(variant >= -1 && variant < NVARIANTS && group_m >= 0, "gemm_set_variant: bad args");
   g_variant = variant;
   g_group_m = group_m;
   return MDEMI_OK;

@@ -420,3 +420,39 @@ def test_space_to_depth_concat_droppath(mf):
     kept = (y - res).abs().sum(1) > 0
     exp = res + br.detach() * 2.0 * kept.float().unsqueeze(1)
     close(y, exp.cpu(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("layouts", ["fwd", "dgrad", "wgrad"])
+def test_gemm_variants_bit_identical(mf, layouts):
+    """Every pipelining variant (and hence the per-shape autotuner's pick) adds
+    the k products in the same order: results must match bit for bit,
+    including split-K and a K that is not a multiple of 32."""
+    from mdemi import _lib as L
+    lib = L.load()
+    M, N, K = 700, 300, 1000
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(N, K, device=DEV)
+    at, bt = a.t().contiguous(), b.t().contiguous()
+    outs = []
+    try:
+        for v in range(6):
+            L.check(lib.mdemi_gemm_set_variant(v, 8), "set_variant")
+            for split in (1, 5):
+                c = torch.empty(M, N, device=DEV)
+                if layouts == "fwd":
+                    mf.gemm(a, b, c, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+                            split_k=split)
+                elif layouts == "dgrad":
+                    mf.gemm(a, bt, c, M, N, K, lda=K, ldb=N, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
+                            split_k=split)
+                else:
+                    mf.gemm(at, bt, c, M, N, K, lda=M, ldb=N, ldc=N, a_layout=L.L_MNCONTIG,
+                            b_layout=L.L_MNCONTIG, split_k=split)
+                outs.append((v, split, c))
+    finally:
+        lib.mdemi_gemm_set_variant(-1, 8)
+    ref = (a.double() @ b.double().t()).float()
+    for v, split, c in outs:
+        close(c, ref, rtol=1e-5 * math.sqrt(K))
+        same = [o for o in outs if o[1] == split][0][2]
+        assert torch.equal(c, same), f"variant {v} split {split} differs bitwise"
