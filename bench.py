@@ -36,8 +36,17 @@ HBM_PEAK_GBS = 8000.0
 
 WORKLOADS = {
     "newcrfs": dict(model="NewCRFs-L07", h=480, w=640, batch=8, max_depth=10.0,
-                    workload="NewCRFs Swin-L (large07) train step, NYU 480x640"),
+                    workload="NewCRFs Swin-L (large07) train step, NYU 480x640",
+                    ref_cfg="json/nyu/newcrfs/newcrfs_github_eval.json"),
+    # BASELINE.json configs[2] / north_star target shape
+    "newcrfs_kitti": dict(model="NewCRFs-L07", h=352, w=1216, batch=8, max_depth=80.0,
+                          workload="NewCRFs Swin-L (large07) train step, KITTI 352x1216",
+                          ref_cfg="json/kitti/newcrfs/newcrfs_github_eval.json"),
 }
+# HBM bytes per launch of the roofline kernel family, from the committed
+# rocprofv3 --pmc passes (tools/pmc_traffic.py; FETCH_SIZE doubled per the
+# gfx950 correction).  None when no profile matches the kernel.
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 
 def parse():
@@ -186,6 +195,18 @@ def gemm_roofline(model, opt, loss_fn, img, gt, ddp):
 KERNEL_NAME = {0: "KCONTIG", 1: "MNCONTIG", 2: "CONV"}
 
 
+def profiled_traffic(regex, workload):
+    try:
+        with open(TRAFFIC_FILE) as f:
+            prof = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ent = prof.get(workload, {})
+    if ent.get("kernel_regex") != regex:
+        return None
+    return ent.get("traffic_bytes_per_launch")
+
+
 def cpu_baseline(model, H, W, budget_s):
     """The oracle (CPU restatement of the reference path, oracle/newcrfs.py) timed on the host
     cores: fp32 forward + SILog + backward + AdamW(clip) step at batch 1, same weights."""
@@ -269,10 +290,12 @@ def main():
         by, dom, tot_fl, tot_t = gemm_roofline(model, opt, loss_fn, img, gt, ddp)
         (al, bl, aop, bop), (fl, t, cnt) = dom
         ach = fl / t / 1e12
+        regex = f"gemm_f32_kernel<{al}, {bl}, {aop}, {bop},"
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": f"gemm_f32_kernel<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}>",
-                "launches": cnt, "avg_launch_us": round(t / cnt * 1e6, 2),
+                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": profiled_traffic(regex, args.model), "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
+                "kernel": f"gemm_f32_kernel<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}> (all pipelining variants)",
+                "kernel_regex": regex, "launches": cnt, "avg_launch_us": round(t / cnt * 1e6, 2),
                 "flops_per_launch": fl / cnt}
         extra["gemm_all"] = {"achieved_tflops": round(tot_fl / tot_t / 1e12, 2), "gemm_ms_per_step": round(tot_t * 1e3, 2),
                              "gemm_tflop_per_step": round(tot_fl / 1e12, 3),
@@ -291,7 +314,7 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights)",
             "config": {"workload": cfg["workload"], "model": cfg["model"], "global_batch": B * world,
                        "per_gpu_batch": B, "image": [H, W], "parallelism": f"dp{world}",
-                       "reference_config": "json/nyu/newcrfs/newcrfs_github_eval.json"},
+                       "reference_config": cfg["ref_cfg"]},
             "roofline": roof, "cpu_baseline": cpu, "loss": round(loss_v, 5), **extra,
         }
         print(json.dumps(line), flush=True)

@@ -1,3 +1,5 @@
+# Round-1 profile set for the default bench workload (run on the GPU box):
+#   kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in their own --pmc passes.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline"
