@@ -101,6 +101,9 @@ typedef struct mdemi_gemm_desc {
   float* preact; int64_t ldpre; int64_t pre_bstride;  /* optional 2nd output: the value
                                       before `act` (and before residual); lets fc1 store
                                       both h and gelu(h) in one pass */
+  float* rowsum_a;                 /* optional [M] output: sum_k A(i,k), A m-contiguous and
+                                      batch 1 -- the bias gradient of a weight-gradient GEMM
+                                      (dW = dY^T X, db = dY^T 1) without a second pass over dY */
 } mdemi_gemm_desc;
 
 size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d);

@@ -59,6 +59,7 @@ struct GemmParams {
   const float* aux; int64_t ldaux, aux_bs;
   const float* res; int64_t ldres, res_bs;
   float* pre; int64_t ldpre, pre_bs;  // optional pre-activation output
+  float* rowsum;   // optional sum_k A(i,k) (A m-contiguous, batch 1): [split][M] partials or [M]
   float* slab;  // split-K partials [split][batch][M][N]
   mdemi_conv_geom cv;
   FastDiv fd_c, fd_kw, fd_ow, fd_oh;  // conv index decomposition
@@ -380,6 +381,20 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
       for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
 
   float4 ra[NQ], rb[NQ];
+  // Row sums of an m-contiguous A (the bias gradient of a weight-gradient
+  // GEMM, dW = dY^T X, db = dY^T 1) accumulated from the staged registers
+  // by the tn == 0 column of workgroups: no second pass over dY.
+  constexpr bool CAN_RSUM = AL == MDEMI_L_MNCONTIG;
+  const bool do_rsum = CAN_RSUM && p.rowsum != nullptr && tn == 0;
+  float4 rsum = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto acc_rsum = [&]() {
+    if (CAN_RSUM && do_rsum) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        rsum.x += ra[q].x; rsum.y += ra[q].y; rsum.z += ra[q].z; rsum.w += ra[q].w;
+      }
+    }
+  };
   const int l31 = lane & 31, h = lane >> 5;
   const int ra0 = wm * 64 + l31, ra1 = ra0 + 32;
   const int rb0 = wn * 64 + l31, rb1 = rb0 + 32;
@@ -389,6 +404,7 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
     lb.load(kt_begin * BK, rb);
     LA::store(smem, t, ra);
     LB::store(smem + FA, t, rb);
+    acc_rsum();
     __syncthreads();
   }
 
@@ -400,6 +416,7 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
       lb.load(kt * BK, rb);
       LA::store(smem, t, ra);
       LB::store(smem + FA, t, rb);
+      acc_rsum();
       __syncthreads();
     } else if (more) {  // issue next tile's global loads early; they land under the MFMAs
       la.load((kt + 1) * BK, ra);
@@ -429,9 +446,30 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
         float* dst = smem + (NBUF == 1 ? 0 : (cur ^ 1)) * (FA + FB);
         LA::store(dst, t, ra);
         LB::store(dst + FA, t, rb);
+        acc_rsum();
       }
       __syncthreads();
       if (NBUF == 2) cur ^= 1;
+    }
+  }
+  if (CAN_RSUM && do_rsum) {  // reduce the 8 k-row groups (t >> 5) through LDS
+    if (!PREF) __syncthreads();
+    float4* red = reinterpret_cast<float4*>(smem);
+    red[t] = rsum;
+    __syncthreads();
+    if (t < 32) {
+      float4 s4 = red[t];
+#pragma unroll
+      for (int g = 1; g < 8; ++g) {
+        const float4 o = red[t + 32 * g];
+        s4.x += o.x; s4.y += o.y; s4.z += o.z; s4.w += o.w;
+      }
+      float* dst = p.rowsum + (p.split > 1 ? (int64_t)sidx * p.M : 0);
+      const int i = bm + 4 * t;
+      if (i + 0 < p.M) dst[i + 0] = s4.x;
+      if (i + 1 < p.M) dst[i + 1] = s4.y;
+      if (i + 2 < p.M) dst[i + 2] = s4.z;
+      if (i + 3 < p.M) dst[i + 3] = s4.w;
     }
   }
 
@@ -541,6 +579,16 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
   }
 }
 
+// rowsum partials [split][M] -> out[M] in split order (deterministic)
+__global__ __launch_bounds__(256) void gemm_rowsum_reduce(const float* __restrict__ part, int split, int M,
+                                                          float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= M) return;
+  float s = 0.f;
+  for (int q = 0; q < split; ++q) s += part[(int64_t)q * M + i];
+  out[i] = s;
+}
+
 using KernelFn = void (*)(GemmParams);
 
 // Variants (tools/gemm_bench.py on the NewCRFs-L07 480x640 bs=8 shapes,
@@ -624,6 +672,9 @@ static int validate(const mdemi_gemm_desc* d) {
     MDEMI_REQUIRE(al16(d->a_layout == MDEMI_L_CONV ? d->A : d->B), "gemm: conv operand must be 16-B aligned");
   }
   MDEMI_REQUIRE(d->bias_mode == MDEMI_BIAS_NONE || d->bias, "gemm: bias pointer missing");
+  MDEMI_REQUIRE(!d->rowsum_a || (d->a_layout == MDEMI_L_MNCONTIG && d->batch == 1),
+                "gemm: rowsum_a needs an m-contiguous A and batch 1");
+  if (d->rowsum_a) MDEMI_REQUIRE(d->rowsum_a != d->C, "gemm: rowsum_a must not alias C");
   // tile-relative 32-bit buffer offsets: 128 rows (or 16 k-rows) of any leading dimension
   const int64_t lim = (int64_t)1 << 21;
   MDEMI_REQUIRE(d->lda < lim && d->ldb < lim && d->ldc < lim && d->ldaux < lim && d->ldres < lim &&
@@ -646,6 +697,7 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant) {
   p.res = d->residual; p.ldres = d->ldres; p.res_bs = d->res_bstride;
   p.cv = d->conv;
   p.pre = d->preact; p.ldpre = d->ldpre; p.pre_bs = d->pre_bstride;
+  p.rowsum = d->rowsum_a;
   // split boundaries in 32-element K chunks whatever the variant's BK
   const int kc = (int)cdiv(d->K, 32);
   const int split = d->split_k < kc ? d->split_k : kc;
@@ -673,6 +725,13 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant) {
 
 using namespace mdemi;
 
+static size_t slab_bytes(const mdemi_gemm_desc* d, const GemmParams& p) {
+  return p.split > 1 ? align_up((size_t)p.split * d->batch * (size_t)d->M * d->N * sizeof(float), 256) : 0;
+}
+static size_t rowsum_bytes(const mdemi_gemm_desc* d, const GemmParams& p) {
+  return (p.split > 1 && d->rowsum_a) ? (size_t)p.split * d->M * sizeof(float) : 0;
+}
+
 static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
   KernelFn fn = pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant);
   if (!fn) {
@@ -682,13 +741,18 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
   }
   GemmParams p;
   fill_params(d, p, variant);
+  float* rowsum_part = nullptr;
   if (p.split > 1) {
-    const size_t need = (size_t)p.split * d->batch * (size_t)d->M * d->N * sizeof(float);
+    const size_t need = slab_bytes(d, p) + rowsum_bytes(d, p);
     if (!d->workspace || (size_t)d->workspace_bytes < need) {
       set_error("gemm: split-K needs %zu workspace bytes", need);
       return MDEMI_EWORKSPACE;
     }
     p.slab = (float*)d->workspace;
+    if (d->rowsum_a) {
+      rowsum_part = (float*)((char*)d->workspace + slab_bytes(d, p));
+      p.rowsum = rowsum_part;
+    }
   }
   const int64_t nblocks = (int64_t)p.tiles_m * p.tiles_n * d->batch * p.split;
   MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
@@ -697,6 +761,9 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
     const int64_t total = (int64_t)d->M * d->N * d->batch;
     const int nb = (int)(cdiv(total, 256) < 4096 ? cdiv(total, 256) : 4096);
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(nb), dim3(256), 0, st, p);
+    if (rowsum_part)
+      hipLaunchKernelGGL(gemm_rowsum_reduce, dim3((unsigned)cdiv(d->M, 256)), dim3(256), 0, st,
+                         (const float*)rowsum_part, p.split, d->M, d->rowsum_a);
   }
   return check_launch("gemm_f32");
 }
@@ -716,6 +783,7 @@ static bool tunable(const mdemi_gemm_desc* d, hipStream_t st) {
   if (d->beta != 0.f) return false;
   const void* c = d->C;
   if (c == d->A || c == d->B || c == d->residual || c == d->aux || c == d->bias) return false;
+  if (d->rowsum_a && (d->rowsum_a == d->A || d->rowsum_a == d->B)) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
   return true;
@@ -756,7 +824,7 @@ extern "C" size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d) {
   GemmParams p;
   fill_params(d, p, 0);  // the split count does not depend on the variant
   if (p.split <= 1) return 0;
-  return (size_t)p.split * d->batch * (size_t)d->M * d->N * sizeof(float);
+  return slab_bytes(d, p) + rowsum_bytes(d, p);
 }
 
 extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {

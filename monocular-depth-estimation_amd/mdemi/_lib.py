@@ -56,6 +56,7 @@ class GemmDesc(ctypes.Structure):
         ("workspace", vp), ("workspace_bytes", i64),
         ("conv", ConvGeom),
         ("preact", vp), ("ldpre", i64), ("pre_bstride", i64),
+        ("rowsum_a", vp),
     ]
 
 

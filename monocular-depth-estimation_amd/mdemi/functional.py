@@ -48,7 +48,7 @@ def _split_for(M, N, K):
 def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE, b_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
-         res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0):
+         res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0, rowsum_a=None):
     d = L.GemmDesc()
     d.M, d.N, d.K, d.batch = M, N, K, batch
     d.A, d.lda, d.a_bstride, d.a_layout, d.a_op = A.data_ptr(), lda, a_bstride, a_layout, a_op
@@ -63,6 +63,8 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
         d.conv = conv
     if preact is not None:
         d.preact, d.ldpre, d.pre_bstride = preact.data_ptr(), ldpre, pre_bstride
+    if rowsum_a is not None:
+        d.rowsum_a = rowsum_a.data_ptr()
     lib = L.load()
     need = lib.mdemi_gemm_workspace_size(ctypes.byref(d))
     if need:
@@ -129,13 +131,16 @@ class _LinearFn(torch.autograd.Function):
                  act=L.ACT_GELU_GRAD if ctx.in_gelu else L.ACT_NONE, aux=x2 if ctx.in_gelu else None,
                  ldaux=K)
             dx = dx.view(ctx.xshape)
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        if want_db:
+            db = torch.empty(N, device=dy.device, dtype=torch.float32)
         if ctx.needs_input_grad[1]:
             dw = torch.empty(N, K, device=dy.device, dtype=torch.float32)
-            # dW[N,K] = dY^T . X  (reduction over the M rows; split-K slabs)
+            # dW[N,K] = dY^T . X  (reduction over the M rows; split-K slabs); db = dY^T 1 rides along
             gemm(dy2, x2, dw, N, K, M, lda=N, ldb=K, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
-                 b_op=L.OP_GELU if ctx.in_gelu else L.OP_NONE)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = colsum(dy2)
+                 b_op=L.OP_GELU if ctx.in_gelu else L.OP_NONE, rowsum_a=db)
+        elif want_db:
+            colsum(dy2, out=db)
         dres = dy if ctx.has_res and ctx.needs_input_grad[3] else None
         return dx, dw, db, dres, None
 
@@ -181,15 +186,17 @@ class _MlpFn(torch.autograd.Function):
         dy2 = _c(dy).reshape(M, N)
         dev = dy.device
         dw2 = torch.empty(N, Hd, device=dev, dtype=torch.float32)
-        gemm(dy2, g, dw2, N, Hd, M, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG)
-        db2 = colsum(dy2) if has_b2 else None
+        db2 = torch.empty(N, device=dev, dtype=torch.float32) if has_b2 else None
+        gemm(dy2, g, dw2, N, Hd, M, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+             rowsum_a=db2)
         dh = torch.empty(M, Hd, device=dev, dtype=torch.float32)
         gemm(dy2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
              act=L.ACT_GELU_GRAD, aux=h, ldaux=Hd)
         del h, g
         dw1 = torch.empty(Hd, K, device=dev, dtype=torch.float32)
-        gemm(dh, x2, dw1, Hd, K, M, lda=Hd, ldb=K, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG)
-        db1 = colsum(dh) if has_b1 else None
+        db1 = torch.empty(Hd, device=dev, dtype=torch.float32) if has_b1 else None
+        gemm(dh, x2, dw1, Hd, K, M, lda=Hd, ldb=K, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+             rowsum_a=db1)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, device=dev, dtype=torch.float32)
@@ -275,16 +282,20 @@ class _Conv2dFn(torch.autograd.Function):
                 gemm(dy, wd, dx, n * h * w, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
                      b_layout=L.L_MNCONTIG, split_k=1,
                      conv=_geom(n, oh, ow, cout, h, w, kh, kw, 1, kh - 1 - pad, L.PAD_ZERO))
+        want_db = has_bias and ctx.needs_input_grad[2]
+        if want_db:
+            db = torch.empty(cout, device=dy.device, dtype=torch.float32)
         if ctx.needs_input_grad[1]:
             dwf = torch.empty(cout, K, device=dy.device, dtype=torch.float32)
             if pointwise:
-                gemm(dy, x, dwf, cout, K, M, lda=cout, ldb=c, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG)
+                gemm(dy, x, dwf, cout, K, M, lda=cout, ldb=c, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+                     rowsum_a=db)
             else:
                 gemm(dy, x, dwf, cout, K, M, lda=cout, ldb=0, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_CONV,
-                     conv=_geom(n, h, w, c, oh, ow, kh, kw, stride, pad, pad_mode))
+                     conv=_geom(n, h, w, c, oh, ow, kh, kw, stride, pad, pad_mode), rowsum_a=db)
             dw = dwf.view(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()
-        if has_bias and ctx.needs_input_grad[2]:
-            db = colsum(dy.reshape(-1, cout))
+        elif want_db:
+            colsum(dy.reshape(-1, cout), out=db)
         return dx, dw, db, None, None, None, None
 
 
@@ -356,8 +367,9 @@ class _PatchEmbedFn(torch.autograd.Function):
         M, K = cols.shape
         dy2 = _c(dy).reshape(M, cout)
         dw = torch.empty(cout, K, device=dy.device, dtype=torch.float32)
-        gemm(dy2, cols, dw, cout, K, M, lda=cout, ldb=K, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG)
-        db = colsum(dy2) if ctx.has_bias else None
+        db = torch.empty(cout, device=dy.device, dtype=torch.float32) if ctx.has_bias else None
+        gemm(dy2, cols, dw, cout, K, M, lda=cout, ldb=K, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+             rowsum_a=db)
         return None, dw.view_as(weight), db
 
 
