@@ -193,6 +193,7 @@ typedef struct mdemi_winattn_desc {
   void* workspace; int64_t workspace_bytes;
 } mdemi_winattn_desc;
 
+size_t mdemi_winattn_fwd_workspace_size(const mdemi_winattn_desc* d);
 int mdemi_winattn_fwd(const mdemi_winattn_desc* d, void* stream);
 size_t mdemi_winattn_bwd_workspace_size(const mdemi_winattn_desc* d);
 int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream);

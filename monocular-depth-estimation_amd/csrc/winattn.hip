@@ -72,6 +72,16 @@ __device__ __forceinline__ float4 ld_tok4(const float* base, int64_t ld, int row
   return make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// all-zero source row for padding tokens (never written)
+__device__ float g_wa_zero[128];
+
+// start of the row that window token data comes from: the token's row, the
+// pad vector (Linear bias) for pad tokens, or zeros (CRF v pads, MFMA padding)
+__device__ __forceinline__ const float* tok_src(const float* base, int64_t ld, int row, const float* pad, bool real) {
+  const float* padsrc = pad ? pad : g_wa_zero;
+  return !real ? g_wa_zero : (row >= 0 ? base + (int64_t)row * ld : padsrc);
+}
+
 __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
   return fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
 }
@@ -92,227 +102,460 @@ struct WinParams {
   float* dsum;     // [nwin][heads][N]  D_i = dO_i . O_i
 };
 
-template <int WS, int HD>
-__global__ __launch_bounds__(64) void winattn_fwd_kernel(WinParams p) {
-  constexpr int N = WS * WS, T = (2 * WS - 1) * (2 * WS - 1), H4 = HD / 4;
-  static_assert(N <= 64, "window too large for one wave");
-  __shared__ float4 Ks[N][H4];
-  __shared__ float4 Vs[N][H4];
-  __shared__ float tab[T];
-  const WinGeom& g = p.g;
-  const int win = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
-  const Win<WS> w(g, win);
-  for (int e = lane; e < N * H4; e += 64) {
-    const int j = e / H4, q4 = e % H4;
-    const int r = w.row(g, j);
-    Ks[j][q4] = ld_tok4(p.k, p.qk_ld, r, p.k_pad, h * HD + 4 * q4);
-    Vs[j][q4] = ld_tok4(p.v, p.v_ld, r, p.v_pad, h * HD + 4 * q4);
+// ---------------------------------------------------------------------------
+// MFMA formulation.  One wave owns one (window, head) item; a workgroup runs
+// WA_WAVES items.  Tokens are padded 49 -> 64 and every product is a 64x64x32
+// (or 32x64x64) tile product on v_mfma_f32_32x32x2_f32.  MFMA lane maps (the
+// k-step s of a 32-deep product uses, in lane half h, element
+// d(s,h) = 8*(s>>2) + 4*h + (s&3), so one float4 register per 4 steps):
+//   A[i][k]: lane l gives A[l&31][d(s, l>>5)]     B[k][j]: lane l gives B[d(s, l>>5)][l&31]
+//   C[i][j]: lane l, reg r holds C[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31]
+// A score tile computed as S^T = K Q^T (rows = keys, columns = queries) leaves
+// one query per lane column, so the softmax over keys is a per-lane reduction
+// plus one cross-half shuffle, and the tile feeds the next product directly
+// as its B operand (k-step s <-> accumulator register s, rows r = s).
+// Relative-position bias and MFMA padding (-inf for keys >= 49) are
+// pre-arranged per head in accumulator order (wa_bias_kernel) and loaded as
+// the accumulator's initial value; the shift mask (-100 across regions) is
+// added only in the last row/column of windows, the only ones it touches.
+// ---------------------------------------------------------------------------
+constexpr int WA_WAVES = 4, WA_NP = 64, WA_HD = 32, WA_N = 49, WA_T = 169;
+typedef float wa_f16x __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float f4c(const float4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ wa_f16x mfma32(float a, float b, wa_f16x c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+// accumulator register r of lane half h -> row within the 32-row tile
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// the lane's 16 operand values of window token `tok` (d = 8g + 4h + c), scaled
+__device__ __forceinline__ void load_frag(float4 (&f)[4], const float* base, int64_t ld, int row, const float* pad,
+                                          bool real, int col0, int h, float scale) {
+  const float* src = tok_src(base, ld, row, pad, real);
+  src = src == g_wa_zero ? src : src + col0;  // the zero row serves every head
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    float4 v = *reinterpret_cast<const float4*>(src + 8 * g4 + 4 * h);
+    v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+    f[g4] = v;
   }
-  for (int e = lane; e < T; e += 64) tab[e] = p.rpb[e * g.heads + h];
-  __syncthreads();
-  const int i = lane;
-  if (i >= N) return;
-  const int ri = w.row(g, i);
-  float* lse_row = p.lse ? p.lse + ((int64_t)win * g.heads + h) * N : nullptr;
-  if (ri < 0) {  // pad query: its output is cropped away
-    if (lse_row) lse_row[i] = INFINITY;
-    return;
-  }
-  const int reg_i = g.shift > 0 ? w.region(g, i) : 0;
-  float4 q[H4];
-  load_row<HD>(q, p.q + (int64_t)ri * p.qk_ld + h * HD);
-#pragma unroll
-  for (int c = 0; c < H4; ++c) { q[c].x *= p.scale; q[c].y *= p.scale; q[c].z *= p.scale; q[c].w *= p.scale; }
-  float s[N];
-  float m = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < H4; ++c) acc += dot4(q[c], Ks[j][c]);
-    acc += tab[rpb_index<WS>(i, j)];
-    if (g.shift > 0 && w.region(g, j) != reg_i) acc += -100.f;
-    s[j] = acc;
-    m = fmaxf(m, acc);
-  }
-  float l = 0.f;
-#pragma unroll
-  for (int j = 0; j < N; ++j) { s[j] = __expf(s[j] - m); l += s[j]; }
-  const float inv = 1.f / l;
-  if (lse_row) lse_row[i] = m + __logf(l);
-  float4 o[H4];
-#pragma unroll
-  for (int c = 0; c < H4; ++c) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    const float pj = s[j] * inv;
-#pragma unroll
-    for (int c = 0; c < H4; ++c) {
-      const float4 v = Vs[j][c];
-      o[c].x = fmaf(pj, v.x, o[c].x); o[c].y = fmaf(pj, v.y, o[c].y);
-      o[c].z = fmaf(pj, v.z, o[c].z); o[c].w = fmaf(pj, v.w, o[c].w);
-    }
-  }
-  float4* dst = reinterpret_cast<float4*>(p.out + (int64_t)ri * p.out_ld + h * HD);
-#pragma unroll
-  for (int c = 0; c < H4; ++c) dst[c] = o[c];
 }
 
-// Backward, split by role so each kernel stages only 2 row-sets in LDS
-// (~13 KB: ~3 waves/SIMD instead of 1) and keeps no score matrix:
-//   P_ij = exp(S_ij - lse_i) from the forward's saved log-sum-exp,
-//   D_i = dO_i . O_i (the identity rowsum(P o dP) = dO . O), dS = P (dP - D).
-// Q-kernel (lane = query i, K/V rows in LDS): dQ_i = scale * sum_j dS_ij k_j,
-//   bias-table gradient through LDS atomics, D_i for the KV-kernel.
-// KV-kernel (lane = key j, scale*Q / dO rows in LDS): dK_j = sum_i dS_ij (scale q_i),
-//   dV_j = sum_i P_ij dO_i; pad keys add into per-window pad sums.
-template <int WS, int HD>
-__global__ __launch_bounds__(64) void winattn_bwd_q_kernel(WinParams p) {
-  constexpr int N = WS * WS, T = (2 * WS - 1) * (2 * WS - 1), H4 = HD / 4;
-  __shared__ float4 Ks[N][H4];
-  __shared__ float4 Vs[N][H4];
-  __shared__ float tab[T];
-  __shared__ float tabg[T];
-  const WinGeom& g = p.g;
-  const int win = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
-  const Win<WS> w(g, win);
-  for (int e = lane; e < N * H4; e += 64) {
-    const int j = e / H4, q4 = e % H4;
-    const int r = w.row(g, j);
-    Ks[j][q4] = ld_tok4(p.k, p.qk_ld, r, p.k_pad, h * HD + 4 * q4);
-    Vs[j][q4] = ld_tok4(p.v, p.v_ld, r, p.v_pad, h * HD + 4 * q4);
-  }
-  for (int e = lane; e < T; e += 64) { tab[e] = p.rpb[e * g.heads + h]; tabg[e] = 0.f; }
-  __syncthreads();
-  const int i = lane;
-  const int64_t rowbase = ((int64_t)win * g.heads + h) * N;
-  if (i < N) {
-    const int ri = w.row(g, i);
-    if (ri >= 0) {
-      const int reg_i = g.shift > 0 ? w.region(g, i) : 0;
-      float4 q[H4], dO[H4];
-      load_row<HD>(q, p.q + (int64_t)ri * p.qk_ld + h * HD);
-      load_row<HD>(dO, p.dout + (int64_t)ri * p.out_ld + h * HD);
-      float D = 0.f;
-      {
-        float4 o[H4];
-        load_row<HD>(o, p.out + (int64_t)ri * p.out_ld + h * HD);
+// init accumulators [a][b] from a per-head bias image laid out [a][b][lane][16]
+__device__ __forceinline__ void load_bias(wa_f16x (&acc)[2][2], const float* img, int lane) {
 #pragma unroll
-        for (int c = 0; c < H4; ++c) {
-          D += dot4(dO[c], o[c]);
-          q[c].x *= p.scale; q[c].y *= p.scale; q[c].z *= p.scale; q[c].w *= p.scale;
-        }
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const float4* src = reinterpret_cast<const float4*>(img + ((a * 2 + b) * 64 + lane) * 16);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const float4 v = src[q4];
+        acc[a][b][4 * q4 + 0] = v.x; acc[a][b][4 * q4 + 1] = v.y;
+        acc[a][b][4 * q4 + 2] = v.z; acc[a][b][4 * q4 + 3] = v.w;
       }
-      const float lse = p.lse[rowbase + i];
-      float4 dq[H4];
-#pragma unroll
-      for (int c = 0; c < H4; ++c) dq[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int j = 0; j < N; ++j) {
-        float s = 0.f, dp = 0.f;
-#pragma unroll
-        for (int c = 0; c < H4; ++c) { s += dot4(q[c], Ks[j][c]); dp += dot4(dO[c], Vs[j][c]); }
-        s += tab[rpb_index<WS>(i, j)];
-        if (g.shift > 0 && w.region(g, j) != reg_i) s += -100.f;
-        const float ds = __expf(s - lse) * (dp - D);
-        atomicAdd(&tabg[rpb_index<WS>(i, j)], ds);
-#pragma unroll
-        for (int c = 0; c < H4; ++c) {
-          const float4 kk = Ks[j][c];
-          dq[c].x = fmaf(ds, kk.x, dq[c].x); dq[c].y = fmaf(ds, kk.y, dq[c].y);
-          dq[c].z = fmaf(ds, kk.z, dq[c].z); dq[c].w = fmaf(ds, kk.w, dq[c].w);
-        }
-      }
-      float4* dst = reinterpret_cast<float4*>(p.dq + (int64_t)ri * p.dqk_ld + h * HD);
-#pragma unroll
-      for (int c = 0; c < H4; ++c)
-        dst[c] = make_float4(dq[c].x * p.scale, dq[c].y * p.scale, dq[c].z * p.scale, dq[c].w * p.scale);
-      p.dsum[rowbase + i] = D;
-    } else {
-      p.dsum[rowbase + i] = 0.f;
     }
-  }
-  __syncthreads();
-  float* P = p.partial + ((int64_t)win * g.heads + h) * (T + 2 * HD);
-  for (int e = lane; e < T; e += 64) P[e] = tabg[e];
+}
+
+// acc[a][b] (+)= sum_s A_a(s) B_b(s) over the 32-deep head dimension
+__device__ __forceinline__ void mma_hd(wa_f16x (&acc)[2][2], const float4 (&fa)[2][4], const float4 (&fb)[2][4]) {
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(f4c(fa[a][g4], c), f4c(fb[b][g4], c), acc[a][b]);
+}
+
+// out[nt] (+)= sum over 64 tokens t of Rows[t][l&31] * Acc[t-tile][nt][reg(t)], i.e. an
+// [32 x 64] x [64 x 32] product whose A comes from a [64][32] LDS row image and whose
+// B is a score tile; token-tile 1 steps with every token >= 56 are skipped (all padding).
+__device__ __forceinline__ void mma_tok(wa_f16x (&out)[2], const float (*rows)[WA_HD], const wa_f16x (&acc)[2][2],
+                                        int l31, int h) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < (t == 0 ? 16 : 12); ++s) {
+      const float a = rows[t * 32 + acc_row(s, h)][l31];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) out[n] = mfma32(a, acc[t][n][s], out[n]);
+    }
+}
+
+struct WaItem {
+  int item, win, hh;
+  bool active;
+};
+__device__ __forceinline__ WaItem wa_item(const WinParams& p, int nitems) {
+  WaItem it;
+  it.item = blockIdx.x * WA_WAVES + (threadIdx.x >> 6);
+  it.active = it.item < nitems;
+  const int i = it.active ? it.item : 0;
+  it.win = i / p.g.heads;
+  it.hh = i % p.g.heads;
+  return it;
+}
+
+// per-wave region ids (shift mask) and "needs mask" flag
+__device__ __forceinline__ bool wa_regions(const WinParams& p, const Win<7>& w, int8_t* reg, int lane) {
+  const bool border = p.g.shift > 0 && (w.wy == p.g.nWh - 1 || w.wx == p.g.nWw - 1);
+  if (border) reg[lane] = lane < WA_N ? (int8_t)w.region(p.g, lane) : (int8_t)0;
+  return border;
 }
 
 template <int WS, int HD>
-__global__ __launch_bounds__(64) void winattn_bwd_kv_kernel(WinParams p) {
-  constexpr int N = WS * WS, T = (2 * WS - 1) * (2 * WS - 1), H4 = HD / 4;
-  __shared__ float4 Qs[N][H4];  // scale * q
-  __shared__ float4 Ds[N][H4];  // dO
-  __shared__ float tab[T];
-  __shared__ float lse_s[N], D_s[N];
-  __shared__ int reg_s[N];
-  __shared__ float padk[HD], padv[HD];
+__global__ __launch_bounds__(256) void winattn_fwd_kernel(WinParams p, const float* __restrict__ biasT, int nitems) {
+  static_assert(WS == 7 && HD == WA_HD, "MFMA window attention is built for 7x7 windows, head_dim 32");
+  __shared__ float Vs[WA_WAVES][WA_NP][WA_HD];
+  __shared__ int8_t regs[WA_WAVES][WA_NP];
   const WinGeom& g = p.g;
-  const int win = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
-  const Win<WS> w(g, win);
-  const int64_t rowbase = ((int64_t)win * g.heads + h) * N;
-  for (int e = lane; e < N * H4; e += 64) {
-    const int i = e / H4, q4 = e % H4;
-    const int r = w.row(g, i);
-    float4 qq = ld_tok4(p.q, p.qk_ld, r, p.q_pad, h * HD + 4 * q4);
-    qq.x *= p.scale; qq.y *= p.scale; qq.z *= p.scale; qq.w *= p.scale;
-    Qs[i][q4] = qq;
-    Ds[i][q4] = r >= 0 ? *reinterpret_cast<const float4*>(p.dout + (int64_t)r * p.out_ld + h * HD + 4 * q4)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l31 = lane & 31, h = lane >> 5;
+  const WaItem it = wa_item(p, nitems);
+  const Win<WS> w(g, it.win);
+  const int col0 = it.hh * HD;
+  for (int e = lane; e < WA_NP * HD / 4; e += 64) {
+    const int tok = e >> 3, c4 = e & 7;
+    const float4 v = tok < WA_N ? ld_tok4(p.v, p.v_ld, w.row(g, tok), p.v_pad, col0 + 4 * c4)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(&Vs[wv][tok][4 * c4]) = v;
   }
-  for (int e = lane; e < T; e += 64) tab[e] = p.rpb[e * g.heads + h];
-  if (lane < N) {
-    lse_s[lane] = p.lse[rowbase + lane];  // +inf for pad queries -> P = 0
-    D_s[lane] = p.dsum[rowbase + lane];
-    reg_s[lane] = g.shift > 0 ? w.region(g, lane) : 0;
-  }
-  if (lane < HD) { padk[lane] = 0.f; padv[lane] = 0.f; }
-  __syncthreads();
-  const int j = lane;
-  if (j < N) {
-    const int rj = w.row(g, j);
-    const int reg_j = reg_s[j];
-    float4 kj[H4], vj[H4], dk[H4], dv[H4];
+  const bool border = wa_regions(p, w, regs[wv], lane);
+  wa_f16x s[2][2];  // S^T [key tile][query tile]
+  load_bias(s, biasT + (size_t)it.hh * 4096, lane);
+  {
+    float4 kf[2][4], qf[2][4];
 #pragma unroll
-    for (int c = 0; c < H4; ++c) {
-      kj[c] = ld_tok4(p.k, p.qk_ld, rj, p.k_pad, h * HD + 4 * c);
-      vj[c] = ld_tok4(p.v, p.v_ld, rj, p.v_pad, h * HD + 4 * c);
-      dk[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-      dv[c] = dk[c];
+    for (int t = 0; t < 2; ++t) {
+      const int tok = t * 32 + l31;
+      const bool real = tok < WA_N;
+      const int row = real ? w.row(g, tok) : -1;
+      load_frag(kf[t], p.k, p.qk_ld, row, p.k_pad, real, col0, h, 1.f);
+      load_frag(qf[t], p.q, p.qk_ld, row, p.q_pad, real, col0, h, p.scale);
     }
-    for (int i = 0; i < N; ++i) {
-      float s = 0.f, dp = 0.f;
+    mma_hd(s, kf, qf);
+  }
+  __syncthreads();  // Vs, regs
+  if (border) {
 #pragma unroll
-      for (int c = 0; c < H4; ++c) { s += dot4(Qs[i][c], kj[c]); dp += dot4(Ds[i][c], vj[c]); }
-      s += tab[rpb_index<WS>(i, j)];
-      if (g.shift > 0 && reg_s[i] != reg_j) s += -100.f;
-      const float pr = __expf(s - lse_s[i]);
-      const float ds = pr * (dp - D_s[i]);
+    for (int n = 0; n < 2; ++n) {
+      const int rq = regs[wv][n * 32 + l31];
 #pragma unroll
-      for (int c = 0; c < H4; ++c) {
-        const float4 qq = Qs[i][c], dd = Ds[i][c];
-        dk[c].x = fmaf(ds, qq.x, dk[c].x); dk[c].y = fmaf(ds, qq.y, dk[c].y);
-        dk[c].z = fmaf(ds, qq.z, dk[c].z); dk[c].w = fmaf(ds, qq.w, dk[c].w);
-        dv[c].x = fmaf(pr, dd.x, dv[c].x); dv[c].y = fmaf(pr, dd.y, dv[c].y);
-        dv[c].z = fmaf(pr, dd.z, dv[c].z); dv[c].w = fmaf(pr, dd.w, dv[c].w);
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (regs[wv][t * 32 + acc_row(r, h)] != rq) s[t][n][r] -= 100.f;
+    }
+  }
+  float lse[2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m = fmaxf(m, s[t][n][r]);
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __expf(s[t][n][r] - m);
+        s[t][n][r] = e;
+        l += e;
+      }
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[t][n][r] *= inv;
+    lse[n] = m + __logf(l);
+  }
+  wa_f16x o[2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[n][r] = 0.f;
+  mma_tok(o, Vs[wv], s, l31, h);  // O^T[d][q] = sum_key V[key][d] P^T[key][q]
+  if (!it.active) return;
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const int q = n * 32 + l31;
+    if (q >= WA_N) continue;
+    const int row = w.row(g, q);
+    if (p.lse && h == 0) p.lse[(int64_t)it.item * WA_N + q] = row >= 0 ? lse[n] : INFINITY;
+    if (row < 0) continue;  // pad query: cropped away
+    float* dst = p.out + (int64_t)row * p.out_ld + col0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      *reinterpret_cast<float4*>(dst + 8 * a + 4 * h) =
+          make_float4(o[n][4 * a], o[n][4 * a + 1], o[n][4 * a + 2], o[n][4 * a + 3]);
+  }
+}
+
+// Backward, query side (lane column = query): recompute P^T, dP^T = V dO^T,
+// dS^T = P^T (dP^T - D), D = rowsum(dO o O); dQ^T = K^T dS^T; bias-table
+// gradient through per-wave LDS atomics.
+template <int WS, int HD>
+__global__ __launch_bounds__(256) void winattn_bwd_q_kernel(WinParams p, const float* __restrict__ biasT, int nitems) {
+  __shared__ float Ks[WA_WAVES][WA_NP][WA_HD];
+  __shared__ float tabg[WA_WAVES][WA_T + 3];
+  __shared__ int8_t regs[WA_WAVES][WA_NP];
+  __shared__ int kidx[WA_NP];
+  const WinGeom& g = p.g;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l31 = lane & 31, h = lane >> 5;
+  const WaItem it = wa_item(p, nitems);
+  const Win<WS> w(g, it.win);
+  const int col0 = it.hh * HD;
+  for (int e = lane; e < WA_NP * HD / 4; e += 64) {
+    const int tok = e >> 3, c4 = e & 7;
+    const float4 v = tok < WA_N ? ld_tok4(p.k, p.qk_ld, w.row(g, tok), p.k_pad, col0 + 4 * c4)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(&Ks[wv][tok][4 * c4]) = v;
+  }
+  for (int e = lane; e < WA_T + 3; e += 64) tabg[wv][e] = 0.f;
+  if (wv == 0) kidx[lane] = lane < WA_N ? (lane / WS) * (2 * WS - 1) + lane % WS : 0;
+  const bool border = wa_regions(p, w, regs[wv], lane);
+  wa_f16x s[2][2], dp[2][2];
+  load_bias(s, biasT + (size_t)it.hh * 4096, lane);
+  float4 qf[2][4];
+  int qrow[2];
+  bool qreal[2];
+  {
+    float4 kf[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int tok = t * 32 + l31;
+      qreal[t] = tok < WA_N;
+      qrow[t] = qreal[t] ? w.row(g, tok) : -1;
+      load_frag(kf[t], p.k, p.qk_ld, qrow[t], p.k_pad, qreal[t], col0, h, 1.f);
+      load_frag(qf[t], p.q, p.qk_ld, qrow[t], p.q_pad, qreal[t], col0, h, p.scale);
+    }
+    mma_hd(s, kf, qf);
+  }
+  float D[2];
+  {
+    float4 vf[2][4], df[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      // dO / O exist only for real (non-pad) query rows: pad and padding queries get 0
+      const bool qo = qreal[t] && qrow[t] >= 0;
+      load_frag(vf[t], p.v, p.v_ld, qrow[t], p.v_pad, qreal[t], col0, h, 1.f);
+      load_frag(df[t], p.dout, p.out_ld, qrow[t], nullptr, qo, col0, h, 1.f);
+      float4 of[4];
+      load_frag(of, p.out, p.out_ld, qrow[t], nullptr, qo, col0, h, 1.f);
+      float part = 0.f;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) part += dot4(df[t][g4], of[g4]);
+      D[t] = part + __shfl_xor(part, 32, 64);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[a][b][r] = 0.f;
+    mma_hd(dp, vf, df);  // dP^T[key][q] = sum_d V[key][d] dO[q][d]
+  }
+  __syncthreads();  // Ks, tabg, kidx, regs
+  float lse[2];
+  int bq[2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const int q = n * 32 + l31;
+    lse[n] = (q < WA_N) ? p.lse[(int64_t)it.item * WA_N + q] : INFINITY;
+    bq[n] = q < WA_N ? (q / WS + WS - 1) * (2 * WS - 1) + q % WS + WS - 1 : -1;
+  }
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const int rq = border ? regs[wv][n * 32 + l31] : 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = t * 32 + acc_row(r, h);
+        float sv = s[t][n][r];
+        if (border && regs[wv][key] != rq) sv -= 100.f;
+        const float ds = __expf(sv - lse[n]) * (dp[t][n][r] - D[n]);
+        dp[t][n][r] = ds;
+        if (bq[n] >= 0 && key < WA_N) atomicAdd(&tabg[wv][bq[n] - kidx[key]], ds);
+      }
+  }
+  wa_f16x dq[2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[n][r] = 0.f;
+  mma_tok(dq, Ks[wv], dp, l31, h);  // dQ^T[d][q] = sum_key K[key][d] dS^T[key][q]
+  if (it.active) {
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int q = n * 32 + l31;
+      if (q >= WA_N) continue;
+      if (h == 0) p.dsum[(int64_t)it.item * WA_N + q] = qrow[n] >= 0 ? D[n] : 0.f;
+      if (qrow[n] < 0) continue;
+      float* dst = p.dq + (int64_t)qrow[n] * p.dqk_ld + col0;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        *reinterpret_cast<float4*>(dst + 8 * a + 4 * h) =
+            make_float4(dq[n][4 * a] * p.scale, dq[n][4 * a + 1] * p.scale, dq[n][4 * a + 2] * p.scale,
+                        dq[n][4 * a + 3] * p.scale);
+    }
+  }
+  __syncthreads();  // tabg complete
+  if (it.active) {
+    float* P = p.partial + (int64_t)it.item * (WA_T + 2 * HD);
+    for (int e = lane; e < WA_T; e += 64) P[e] = tabg[wv][e];
+  }
+}
+
+// Backward, key side (lane column = key): recompute P = exp(S - lse) with
+// S = Q K^T (rows = queries), dP = dO V^T, dS = P (dP - D);
+// dV^T = dO^T P, dK^T = (scale Q)^T dS.  Pad keys fold into per-item sums.
+template <int WS, int HD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void winattn_bwd_kv_kernel(WinParams p, const float* __restrict__ biasN, int nitems) {
+  __shared__ float Qs[WA_WAVES][WA_NP][WA_HD];  // scale * q
+  __shared__ float Ds[WA_WAVES][WA_NP][WA_HD];  // dO
+  __shared__ float lse_s[WA_WAVES][WA_NP], D_s[WA_WAVES][WA_NP];
+  __shared__ int8_t regs[WA_WAVES][WA_NP];
+  __shared__ float padk[WA_WAVES][WA_HD], padv[WA_WAVES][WA_HD];
+  const WinGeom& g = p.g;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l31 = lane & 31, h = lane >> 5;
+  const WaItem it = wa_item(p, nitems);
+  const Win<WS> w(g, it.win);
+  const int col0 = it.hh * HD;
+  for (int e = lane; e < WA_NP * HD / 4; e += 64) {
+    const int tok = e >> 3, c4 = e & 7;
+    const int row = tok < WA_N ? w.row(g, tok) : -1;
+    float4 qv = tok < WA_N ? ld_tok4(p.q, p.qk_ld, row, p.q_pad, col0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    qv.x *= p.scale; qv.y *= p.scale; qv.z *= p.scale; qv.w *= p.scale;
+    *reinterpret_cast<float4*>(&Qs[wv][tok][4 * c4]) = qv;
+    *reinterpret_cast<float4*>(&Ds[wv][tok][4 * c4]) =
+        row >= 0 ? *reinterpret_cast<const float4*>(p.dout + (int64_t)row * p.out_ld + col0 + 4 * c4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  {
+    const bool qr = lane < WA_N;
+    lse_s[wv][lane] = qr ? p.lse[(int64_t)it.item * WA_N + lane] : INFINITY;  // +inf: P = 0
+    D_s[wv][lane] = qr ? p.dsum[(int64_t)it.item * WA_N + lane] : 0.f;
+  }
+  if (lane < HD) { padk[wv][lane] = 0.f; padv[wv][lane] = 0.f; }
+  const bool border = wa_regions(p, w, regs[wv], lane);
+  wa_f16x s[2][2], dp[2][2];  // [query tile][key tile]
+  load_bias(s, biasN + (size_t)it.hh * 4096, lane);
+  int krow[2];
+  bool kreal[2];
+  {
+    float4 qf[2][4], kf[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int tok = t * 32 + l31;
+      kreal[t] = tok < WA_N;
+      krow[t] = kreal[t] ? w.row(g, tok) : -1;
+      load_frag(qf[t], p.q, p.qk_ld, krow[t], p.q_pad, kreal[t], col0, h, p.scale);
+      load_frag(kf[t], p.k, p.qk_ld, krow[t], p.k_pad, kreal[t], col0, h, 1.f);
+    }
+    mma_hd(s, qf, kf);  // S[q][key]
+  }
+  {
+    float4 df[2][4], vf[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      load_frag(df[t], p.dout, p.out_ld, krow[t], nullptr, kreal[t] && krow[t] >= 0, col0, h, 1.f);
+      load_frag(vf[t], p.v, p.v_ld, krow[t], p.v_pad, kreal[t], col0, h, 1.f);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[a][b][r] = 0.f;
+    mma_hd(dp, df, vf);  // dP[q][key]
+  }
+  __syncthreads();  // Qs, Ds, lse_s, D_s, regs, pads
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const int rk = border ? regs[wv][n * 32 + l31] : 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = t * 32 + acc_row(r, h);
+        float sv = s[t][n][r];
+        if (border && regs[wv][q] != rk) sv -= 100.f;
+        const float pr = __expf(sv - lse_s[wv][q]);
+        s[t][n][r] = pr;
+        dp[t][n][r] = pr * (dp[t][n][r] - D_s[wv][q]);
+      }
+  }
+  // dV first, then dK: P dies before the dK accumulators go live
+  auto store_grad = [&](const wa_f16x (&gacc)[2], float* gbase, int64_t gld, float* padacc) {
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      if (!it.active || !kreal[n]) continue;
+      if (krow[n] >= 0) {
+        float* dst = gbase + (int64_t)krow[n] * gld + col0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+          *reinterpret_cast<float4*>(dst + 8 * a + 4 * h) =
+              make_float4(gacc[n][4 * a], gacc[n][4 * a + 1], gacc[n][4 * a + 2], gacc[n][4 * a + 3]);
+      } else {  // pad key: its k / v were the Linear bias (or 0) -> sum into the bias gradient
+#pragma unroll
+        for (int r = 0; r < 16; ++r) atomicAdd(&padacc[acc_row(r, h)], gacc[n][r]);
       }
     }
-    if (rj >= 0) {
-      float4* dkd = reinterpret_cast<float4*>(p.dk + (int64_t)rj * p.dqk_ld + h * HD);
-      float4* dvd = reinterpret_cast<float4*>(p.dv + (int64_t)rj * p.dv_ld + h * HD);
+  };
+  {
+    wa_f16x dv[2];
 #pragma unroll
-      for (int c = 0; c < H4; ++c) { dkd[c] = dk[c]; dvd[c] = dv[c]; }
-    } else {
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int c = 0; c < H4; ++c) {
-        atomicAdd(&padk[4 * c + 0], dk[c].x); atomicAdd(&padk[4 * c + 1], dk[c].y);
-        atomicAdd(&padk[4 * c + 2], dk[c].z); atomicAdd(&padk[4 * c + 3], dk[c].w);
-        atomicAdd(&padv[4 * c + 0], dv[c].x); atomicAdd(&padv[4 * c + 1], dv[c].y);
-        atomicAdd(&padv[4 * c + 2], dv[c].z); atomicAdd(&padv[4 * c + 3], dv[c].w);
-      }
-    }
+      for (int r = 0; r < 16; ++r) dv[n][r] = 0.f;
+    mma_tok(dv, Ds[wv], s, l31, h);  // dV^T[d][key] = sum_q dO[q][d] P[q][key]
+    store_grad(dv, p.dv, p.dv_ld, padv[wv]);
+  }
+  {
+    wa_f16x dk[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dk[n][r] = 0.f;
+    mma_tok(dk, Qs[wv], dp, l31, h);  // dK^T[d][key] = sum_q (scale q)[q][d] dS[q][key]
+    store_grad(dk, p.dk, p.dqk_ld, padk[wv]);
   }
   __syncthreads();
-  float* P = p.partial + ((int64_t)win * g.heads + h) * (T + 2 * HD);
-  if (lane < HD) { P[T + lane] = padk[lane]; P[T + HD + lane] = padv[lane]; }
+  if (it.active && lane < HD) {
+    float* P = p.partial + (int64_t)it.item * (WA_T + 2 * HD);
+    P[WA_T + lane] = padk[wv][lane];
+    P[WA_T + HD + lane] = padv[wv][lane];
+  }
+}
+
+// Per-head bias images in accumulator order [a][b][lane][r] (a, b = 32-row /
+// 32-column tiles): T (rows = keys, cols = queries) for the forward and the
+// query-side backward, N (rows = queries, cols = keys) for the key side.
+// value = table[rpb_index(q, key)][head]; -inf for MFMA-padding keys (>= 49),
+// 0 for padding queries.
+__global__ __launch_bounds__(256) void wa_bias_kernel(const float* __restrict__ rpb, int heads, float* biasT,
+                                                      float* biasN) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= heads * 4096) return;
+  const int hh = e >> 12, rem = e & 4095;
+  const int tile = rem >> 10, lane = (rem >> 4) & 63, r = rem & 15;
+  const int row = (tile >> 1) * 32 + acc_row(r, lane >> 5), col = (tile & 1) * 32 + (lane & 31);
+  auto val = [&](int q, int key) {
+    if (key >= WA_N) return -INFINITY;
+    if (q >= WA_N) return 0.f;
+    return rpb[rpb_index<7>(q, key) * heads + hh];
+  };
+  if (biasT) biasT[e] = val(col, row);
+  if (biasN) biasN[e] = val(row, col);
 }
 
 // sums[h][t] (column sums over windows of partial[win][h][T + 2*HD]) ->
@@ -360,25 +603,46 @@ static int make_params(const mdemi_winattn_desc* d, WinParams& p, int& nwin) {
 
 using namespace mdemi;
 
+static int wa_items(const mdemi_winattn_desc* d, int nwin) { return nwin * d->heads; }
+static size_t wa_bias_bytes(const mdemi_winattn_desc* d) { return (size_t)d->heads * 4096 * sizeof(float); }
+
+extern "C" size_t mdemi_winattn_fwd_workspace_size(const mdemi_winattn_desc* d) {
+  WinParams p;
+  int nwin;
+  if (make_params(d, p, nwin)) return 0;
+  return wa_bias_bytes(d);
+}
+
 extern "C" int mdemi_winattn_fwd(const mdemi_winattn_desc* d, void* stream) {
   WinParams p;
   int nwin;
   int rc = make_params(d, p, nwin);
   if (rc) return rc;
   MDEMI_REQUIRE(d->out, "winattn_fwd: null out");
-  hipLaunchKernelGGL((winattn_fwd_kernel<7, 32>), dim3(nwin, d->heads), dim3(64), 0, (hipStream_t)stream, p);
+  if (!d->workspace || (size_t)d->workspace_bytes < wa_bias_bytes(d)) {
+    set_error("winattn_fwd: needs %zu workspace bytes", wa_bias_bytes(d));
+    return MDEMI_EWORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  float* biasT = (float*)d->workspace;
+  hipLaunchKernelGGL(wa_bias_kernel, dim3(d->heads * 16), dim3(256), 0, st, d->rpb_table, d->heads, biasT,
+                     (float*)nullptr);
+  const int nitems = wa_items(d, nwin);
+  hipLaunchKernelGGL((winattn_fwd_kernel<7, 32>), dim3(cdiv(nitems, WA_WAVES)), dim3(64 * WA_WAVES), 0, st, p,
+                     (const float*)biasT, nitems);
   return check_launch("winattn_fwd");
 }
 
-// workspace: [partials nwin x heads*R | D nwin x heads x N | sums heads*R | colsum scratch]
-static size_t wa_part_bytes(int nwin, int heads, int R) { return align_up((size_t)nwin * heads * R * 4, 256); }
-static size_t wa_dsum_bytes(int nwin, int heads, int N) { return align_up((size_t)nwin * heads * N * 4, 256); }
+// workspace: [partials items x R | D items x N | bias T | bias N | sums heads*R | colsum scratch]
+static size_t wa_part_bytes(int items, int R) { return align_up((size_t)items * R * 4, 256); }
+static size_t wa_dsum_bytes(int items) { return align_up((size_t)items * WA_N * 4, 256); }
 extern "C" size_t mdemi_winattn_bwd_workspace_size(const mdemi_winattn_desc* d) {
   WinParams p;
   int nwin;
   if (make_params(d, p, nwin)) return 0;
-  const int R = (2 * d->window - 1) * (2 * d->window - 1) + 2 * d->head_dim;
-  return wa_part_bytes(nwin, d->heads, R) + wa_dsum_bytes(nwin, d->heads, d->window * d->window) +
+  const int R = WA_T + 2 * WA_HD;
+  const int items = wa_items(d, nwin);
+  return wa_part_bytes(items, R) + wa_dsum_bytes(items) + 2 * wa_bias_bytes(d) +
          align_up((size_t)d->heads * R * 4, 256) + colsum_ws_bytes(nwin, (int64_t)d->heads * R);
 }
 
@@ -396,12 +660,19 @@ extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
     return MDEMI_EWORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
-  const int R = 13 * 13 + 64;
-  p.dsum = (float*)((char*)d->workspace + wa_part_bytes(nwin, d->heads, R));
-  hipLaunchKernelGGL((winattn_bwd_q_kernel<7, 32>), dim3(nwin, d->heads), dim3(64), 0, st, p);
-  hipLaunchKernelGGL((winattn_bwd_kv_kernel<7, 32>), dim3(nwin, d->heads), dim3(64), 0, st, p);
-  float* sums = (float*)((char*)p.dsum + wa_dsum_bytes(nwin, d->heads, 49));
+  const int R = WA_T + 2 * WA_HD;
+  const int items = wa_items(d, nwin);
+  char* ws = (char*)d->workspace;
+  p.partial = (float*)ws;
+  p.dsum = (float*)(ws + wa_part_bytes(items, R));
+  float* biasT = (float*)((char*)p.dsum + wa_dsum_bytes(items));
+  float* biasN = (float*)((char*)biasT + wa_bias_bytes(d));
+  float* sums = (float*)((char*)biasN + wa_bias_bytes(d));
   void* cws = (char*)sums + align_up((size_t)d->heads * R * 4, 256);
+  hipLaunchKernelGGL(wa_bias_kernel, dim3(d->heads * 16), dim3(256), 0, st, d->rpb_table, d->heads, biasT, biasN);
+  const dim3 grid((unsigned)cdiv(items, WA_WAVES)), block(64 * WA_WAVES);
+  hipLaunchKernelGGL((winattn_bwd_q_kernel<7, 32>), grid, block, 0, st, p, (const float*)biasT, items);
+  hipLaunchKernelGGL((winattn_bwd_kv_kernel<7, 32>), grid, block, 0, st, p, (const float*)biasN, items);
   int rc2 = colsum_launch(p.partial, nwin, (int64_t)d->heads * R, (int64_t)d->heads * R, sums, 0, cws, st);
   if (rc2) return rc2;
   hipLaunchKernelGGL((winattn_bwd_scatter<7, 32>), dim3((d->heads * R + 255) / 256), dim3(256), 0, st, sums, d->heads,

@@ -447,7 +447,10 @@ class _WindowAttnFn(torch.autograd.Function):
         nwin = B * (-(-H // ws)) * (-(-W // ws))
         lse = torch.empty(nwin, heads, ws * ws, device=qk.device, dtype=torch.float32)
         d.lse = lse.data_ptr()
-        L.check(L.load().mdemi_winattn_fwd(ctypes.byref(d), L.stream()), "winattn_fwd")
+        lib = L.load()
+        ws_f = L.workspace(lib.mdemi_winattn_fwd_workspace_size(ctypes.byref(d)), qk.device)
+        d.workspace, d.workspace_bytes = ws_f.data_ptr(), ws_f.numel()
+        L.check(lib.mdemi_winattn_fwd(ctypes.byref(d), L.stream()), "winattn_fwd")
         ctx.save_for_backward(qk, qk_bias, v, v_bias, rpb, out, lse)
         ctx.geom = geom
         ctx.has_qkb = qk_bias is not None
