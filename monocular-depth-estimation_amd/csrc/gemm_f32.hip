@@ -565,28 +565,46 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 }
 
 // Deterministic split-K combine + epilogue: sums slabs in split order.
-__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
+// Deterministic split-K combine + epilogue: sums slabs in split order, four
+// consecutive columns per thread when N % 4 == 0; also folds the row-sum
+// partials [split][M] of a weight-gradient GEMM (bias gradient) in the same launch.
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const float* __restrict__ rs_part,
+                                                          float* __restrict__ rs_out) {
   const int64_t MN = (int64_t)p.M * p.N;
-  const int64_t total = MN * p.batch;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int b = (int)(e / MN);
-    const int64_t rem = e - (int64_t)b * MN;
+  const bool quad = (p.N & 3) == 0;
+  const int64_t units = quad ? MN / 4 : MN;
+  const int64_t total = units * p.batch;
+  const int64_t slab_stride = (int64_t)p.batch * MN;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gstride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = gid; e < total; e += gstride) {
+    const int b = (int)(e / units);
+    const int64_t u = e - (int64_t)b * units;
+    const int64_t rem = quad ? 4 * u : u;
     const int i = (int)(rem / p.N), j = (int)(rem - (int64_t)i * p.N);
-    float s = 0.f;
-    for (int q = 0; q < p.split; ++q) s += p.slab[((int64_t)q * p.batch + b) * MN + rem];
-    p.C[(int64_t)b * p.c_bs + (int64_t)i * p.ldc + j] = epilogue_value(p, b, i, j, s);
+    const float* src = p.slab + (int64_t)b * MN + rem;
+    float* dst = p.C + (int64_t)b * p.c_bs + (int64_t)i * p.ldc + j;
+    if (quad) {
+      float4 acc = *reinterpret_cast<const float4*>(src);
+      for (int q = 1; q < p.split; ++q) {
+        const float4 t = *reinterpret_cast<const float4*>(src + q * slab_stride);
+        acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+      }
+      dst[0] = epilogue_value(p, b, i, j, acc.x);
+      dst[1] = epilogue_value(p, b, i, j + 1, acc.y);
+      dst[2] = epilogue_value(p, b, i, j + 2, acc.z);
+      dst[3] = epilogue_value(p, b, i, j + 3, acc.w);
+    } else {
+      float acc = src[0];
+      for (int q = 1; q < p.split; ++q) acc += src[q * slab_stride];
+      dst[0] = epilogue_value(p, b, i, j, acc);
+    }
   }
-}
-
-// rowsum partials [split][M] -> out[M] in split order (deterministic)
-__global__ __launch_bounds__(256) void gemm_rowsum_reduce(const float* __restrict__ part, int split, int M,
-                                                          float* __restrict__ out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= M) return;
-  float s = 0.f;
-  for (int q = 0; q < split; ++q) s += part[(int64_t)q * M + i];
-  out[i] = s;
+  if (rs_part)
+    for (int64_t i = gid; i < p.M; i += gstride) {
+      float acc = rs_part[i];
+      for (int q = 1; q < p.split; ++q) acc += rs_part[(int64_t)q * p.M + i];
+      rs_out[i] = acc;
+    }
 }
 
 using KernelFn = void (*)(GemmParams);
@@ -758,12 +776,10 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
   MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
   hipLaunchKernelGGL(fn, dim3((unsigned)nblocks), dim3(GTHREADS), 0, st, p);
   if (p.split > 1) {
-    const int64_t total = (int64_t)d->M * d->N * d->batch;
+    const int64_t total = (int64_t)d->M * d->N * d->batch / ((d->N & 3) == 0 ? 4 : 1);
     const int nb = (int)(cdiv(total, 256) < 4096 ? cdiv(total, 256) : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(nb), dim3(256), 0, st, p);
-    if (rowsum_part)
-      hipLaunchKernelGGL(gemm_rowsum_reduce, dim3((unsigned)cdiv(d->M, 256)), dim3(256), 0, st,
-                         (const float*)rowsum_part, p.split, d->M, d->rowsum_a);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(nb), dim3(256), 0, st, p, (const float*)rowsum_part,
+                       rowsum_part ? d->rowsum_a : (float*)nullptr);
   }
   return check_launch("gemm_f32");
 }

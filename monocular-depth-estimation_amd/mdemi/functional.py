@@ -333,7 +333,8 @@ class _HeadConvFn(torch.autograd.Function):
 
 def conv2d_nhwc(x, weight, bias=None, stride=1, pad=0, pad_mode=L.PAD_ZERO, act=L.ACT_NONE):
     if weight.shape[0] == 1 and stride == 1 and pad_mode == L.PAD_ZERO and act == L.ACT_NONE and \
-            2 * pad == weight.shape[-1] - 1 and x.shape[-1] % 4 == 0:
+            2 * pad == weight.shape[-1] - 1 and weight.shape[-1] <= 3 and x.shape[-1] % 4 == 0 and \
+            x.shape[-1] <= 128:
         return _HeadConvFn.apply(x, weight, bias)
     return _Conv2dFn.apply(x, weight, bias, stride, pad, pad_mode, act)
 
