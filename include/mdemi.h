@@ -74,6 +74,9 @@ int mdemi_version(void);
 #define MDEMI_ACT_LEAKY 3      /* negative slope 0.01 (nn.LeakyReLU default) */
 #define MDEMI_ACT_GELU_GRAD 4  /* out = acc * gelu'(aux[i][j])                 */
 #define MDEMI_ACT_SIGMOID 5
+#define MDEMI_ACT_SILU 6       /* x * sigmoid(x) (nn.SiLU: decoder_v8.py:24; EfficientNet swish) */
+#define MDEMI_ACT_RELU_GRAD 7  /* out = acc * [aux[i][j] > 0]                  */
+#define MDEMI_ACT_SILU_GRAD 8  /* out = acc * silu'(aux[i][j])                 */
 /* conv padding modes */
 #define MDEMI_PAD_ZERO 0
 #define MDEMI_PAD_REPLICATE 1
@@ -81,7 +84,9 @@ int mdemi_version(void);
 typedef struct mdemi_conv_geom {
   int32_t n, h, w, c;       /* input activation, NHWC */
   int32_t oh, ow;           /* output spatial size */
-  int32_t kh, kw, stride, pad;
+  int32_t kh, kw, stride, pad;  /* pad = top/left padding; may be negative (a crop,
+                                  the dgrad of a padded 1x1 conv, unet_adaptive_bins.py:32);
+                                  bottom/right padding follows from oh/ow (TF 'same') */
   int32_t pad_mode;         /* MDEMI_PAD_* */
   int32_t _reserved;
 } mdemi_conv_geom;

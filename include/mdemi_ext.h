@@ -1,0 +1,137 @@
+/*
+ * mdemi_ext.h — second part of the libmdemi.so C ABI: the ops of the AdaBins
+ * and Depthformer-v8 rows of the hot path and the
+ * evaluation metrics (A19).  Same conventions as mdemi.h: fp32 device
+ * pointers owned by the caller, channels-last activations, `stream` is a
+ * hipStream_t passed as void*, 0 / negative MDEMI_E* return, scratch through
+ * *_workspace_size() queries, no allocation, no synchronisation.
+ *
+ * Reference call sites are cited per entry point (paths relative to the
+ * reference root).  EfficientNet-B5 itself is third-party
+ * (rwightman/gen-efficientnet-pytorch `tf_efficientnet_b5_ap`, fetched by
+ * torch.hub at unet_adaptive_bins.py:129 / depthformer_v8.py:89); its ops are
+ * restated from that published architecture.
+ */
+#ifndef MDEMI_EXT_H
+#define MDEMI_EXT_H
+
+#include "mdemi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Depthwise KxK convolution over NHWC (groups == C, no bias): the MBConv /  */
+/* DepthwiseSeparable conv_dw of EfficientNet-B5 (encoder walked at          */
+/* unet_adaptive_bins.py:65-73, depthformer_v8.py:15-24).  w is the          */
+/* reference layout [C][1][K][K].  pad_t / pad_l are the top / left padding; */
+/* the bottom / right padding follows from OH / OW, which is how TF 'same'   */
+/* padding (asymmetric for stride 2) is expressed.                           */
+/* ------------------------------------------------------------------------ */
+int mdemi_dwconv_fwd(const float* x, const float* w, float* y, int32_t N, int32_t H, int32_t W, int32_t C,
+                     int32_t K, int32_t stride, int32_t pad_t, int32_t pad_l, int32_t OH, int32_t OW,
+                     void* stream);
+size_t mdemi_dwconv_bwd_workspace_size(int32_t N, int32_t C, int32_t K, int32_t OH, int32_t OW);
+/* dx and/or dw may be NULL to skip that gradient; dw is overwritten. */
+int mdemi_dwconv_bwd(const float* dy, const float* x, const float* w, float* dx, float* dw, int32_t N,
+                     int32_t H, int32_t W, int32_t C, int32_t K, int32_t stride, int32_t pad_t, int32_t pad_l,
+                     int32_t OH, int32_t OW, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Per-(image, channel) spatial reductions and channel scaling over NHWC:    */
+/* global average pooling and the gate of EfficientNet's SqueezeExcite,      */
+/* torch.mean(aux, dim=1) (decoder_v8.py:161).                               */
+/*   out[n][c] = scale * sum_p a[n][p][c] * (b ? b[n][p][c] : 1)             */
+/*   y[n][p][c] = x[n][p][c] * g[n][c] + (add ? add[n][c] : 0)               */
+/* ------------------------------------------------------------------------ */
+size_t mdemi_spatial_reduce_workspace_size(int32_t N, int64_t HW, int32_t C);
+int mdemi_spatial_reduce(const float* a, const float* b, float* out, int32_t N, int64_t HW, int32_t C,
+                         float scale, void* workspace, void* stream);
+int mdemi_chan_scale(const float* x, const float* g, const float* add, float* y, int32_t N, int64_t HW,
+                     int32_t C, void* stream);
+
+/* SqueezeExcite gate MLP (conv_reduce 1x1 + bias, swish, conv_expand 1x1 +  */
+/* bias, sigmoid) on pooled [N][C]; wr [R][C], we [C][R].  hid receives the  */
+/* pre-activation of conv_reduce [N][R] (saved for the backward).            */
+int mdemi_se_gate_fwd(const float* pooled, const float* wr, const float* br, const float* we, const float* be,
+                      float* hid, float* gate, int32_t N, int32_t C, int32_t R, void* stream);
+/* dgate [N][C] -> dpooled [N][C] and the four parameter gradients (overwritten). */
+size_t mdemi_se_gate_bwd_workspace_size(int32_t N, int32_t C, int32_t R);
+int mdemi_se_gate_bwd(const float* pooled, const float* wr, const float* we, const float* hid,
+                      const float* gate, const float* dgate, float* dpooled, float* dwr, float* dbr, float* dwe,
+                      float* dbe, int32_t N, int32_t C, int32_t R, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Row softmax with a pre-scale, y = softmax(scale * x) along the last dim:  */
+/* attention probabilities of nn.TransformerEncoderLayer (layers.py:8-9),    */
+/* PreNormLunaBlock (luna_layer.py:213-215, 244-246), SelfAttentionBlock     */
+/* (self_attention.py:72-74).  Backward: dx = scale * y * (dy - <dy, y>).    */
+/* ------------------------------------------------------------------------ */
+int mdemi_softmax_fwd(const float* x, float* y, int64_t rows, int32_t cols, float scale, void* stream);
+int mdemi_softmax_bwd(const float* y, const float* dy, float* dx, int64_t rows, int32_t cols, float scale,
+                      int32_t accumulate, void* stream);
+
+/* Inverted dropout with a counter-based mask: y = x * keep(seed, offset+i) / (1-p).
+ * The mask is a pure function of (seed, offset, i), so the backward is the
+ * same call on dy (nn.Dropout in layers.py:8, luna_layer.py:172-173,
+ * feed_forward.py:26, decoder_v8.py:84,87).  p == 0 is a copy. */
+int mdemi_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, uint64_t offset, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Channels-last adaptive-bin head: logits [B][HW][K] (the 1x1 conv_out /    */
+/* bin_predictor output, unet_adaptive_bins.py:88-91,97, decoder_v8.py:      */
+/* 158-159), pred[b][p] = sum_k softmax(logits)[k] * centers[b][k]            */
+/* (unet_adaptive_bins.py:107, depthformer_v8.py:73).  stats [B][HW][2] =    */
+/* (max, 1/sum) for the backward.                                            */
+/* ------------------------------------------------------------------------ */
+int mdemi_binhead_nhwc_fwd(const float* logits, const float* centers, float* pred, float* stats, int32_t B,
+                           int64_t HW, int32_t K, void* stream);
+size_t mdemi_binhead_nhwc_bwd_workspace_size(int32_t B, int64_t HW, int32_t K);
+int mdemi_binhead_nhwc_bwd(const float* logits, const float* centers, const float* pred, const float* stats,
+                           const float* dpred, float* dlogits, float* dcenters, int32_t B, int64_t HW, int32_t K,
+                           void* workspace, void* stream);
+
+/* Bin widths -> edges -> centres (unet_adaptive_bins.py:99-105 with         */
+/* miniViT.py:38-46; depthformer_v8.py:62-66 with decoder_v8.py:163-166):     */
+/*   w = act(raw) (mode 0: relu(x)+0.1, 1: elu(x, 0.1)+0.1), wn = w / sum w,  */
+/*   edges = cumsum(pad((max-min)*wn, (1,0), min)), centres = mid-points.    */
+/* widths_n [B][K] (normalised widths, AdaBins' bin_widths_normed) and        */
+/* edges [B][K+1] may be NULL.  Backward: dcenters (+ dedges, dwidths_n,    */
+/* each may be NULL) -> draw.                                                */
+#define MDEMI_BINS_RELU 0
+#define MDEMI_BINS_ELU 1
+int mdemi_bins_fwd(const float* raw, float* widths_n, float* edges, float* centers, int32_t B, int32_t K,
+                   int32_t mode, float min_val, float max_val, void* stream);
+int mdemi_bins_bwd(const float* raw, const float* dcenters, const float* dedges, const float* dwidths_n,
+                   float* draw, int32_t B, int32_t K, int32_t mode, float min_val, float max_val, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Layout helpers                                                            */
+/* ------------------------------------------------------------------------ */
+/* NCHW -> NHWC with the channel dim zero-padded to Cp >= C (the 3-channel    */
+/* image feeding EfficientNet's conv_stem through the implicit-GEMM conv).   */
+int mdemi_nchw_to_nhwc_pad(const float* x, float* y, int32_t N, int32_t C, int64_t HW, int32_t Cp, void* stream);
+/* Adjoint of replicate padding by p (padding_mode="replicate",              */
+/* layer_utils.py:18-22): dx[n][y][x] = sum of dxp over the padded positions */
+/* that clamp to (y, x).  dxp is [N][H+2p][W+2p][C].                          */
+int mdemi_pad_fold_replicate(const float* dxp, float* dx, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p,
+                             void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Evaluation metrics on the GPU (utils/depth_utils.py:4-54): per image,     */
+/* over valid = crop rectangle [y0,y1) x [x0,x1) & gt > min_depth &          */
+/* gt < max_depth, the 9 metrics of tcompute_errors in this order:           */
+/*   a1, a2, a3, abs_rel, sq_rel, rmse, rmse_log, silog, log_10              */
+/* plus the valid-pixel count: out [B][10] (fp64).  clamp_pred != 0 clamps   */
+/* pred into [min_depth, max_depth] first.                                   */
+/* ------------------------------------------------------------------------ */
+size_t mdemi_depth_metrics_workspace_size(int32_t B, int32_t H, int32_t W);
+int mdemi_depth_metrics(const float* pred, const float* gt, int32_t B, int32_t H, int32_t W, int32_t y0,
+                        int32_t y1, int32_t x0, int32_t x1, float min_depth, float max_depth, int32_t clamp_pred,
+                        double* out, void* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDEMI_EXT_H */

@@ -78,6 +78,11 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return fmaf(x * 0.39894228040143268f, e, cdf);
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
+__device__ __forceinline__ float silu_grad_f(float x) {
+  const float s = sigmoid_f(x);
+  return fmaf(x * s, 1.f - s, s);
+}
 
 __device__ __forceinline__ float apply_act(int act, float v) {
   switch (act) {
@@ -85,6 +90,7 @@ __device__ __forceinline__ float apply_act(int act, float v) {
     case MDEMI_ACT_RELU: return v > 0.f ? v : 0.f;
     case MDEMI_ACT_LEAKY: return v > 0.f ? v : 0.01f * v;
     case MDEMI_ACT_SIGMOID: return sigmoid_f(v);
+    case MDEMI_ACT_SILU: return silu_f(v);
     default: return v;
   }
 }
@@ -95,7 +101,20 @@ __device__ __forceinline__ float act_grad(int act, float x, float y) {
     case MDEMI_ACT_RELU: return y > 0.f ? 1.f : 0.f;
     case MDEMI_ACT_LEAKY: return x > 0.f ? 1.f : 0.01f;
     case MDEMI_ACT_SIGMOID: return y * (1.f - y);
+    case MDEMI_ACT_SILU: return silu_grad_f(x);
     default: return 1.f;
+  }
+}
+
+// epilogue multipliers of the *_GRAD codes: act'(aux)
+__device__ __forceinline__ bool is_grad_act(int act) {
+  return act == MDEMI_ACT_GELU_GRAD || act == MDEMI_ACT_RELU_GRAD || act == MDEMI_ACT_SILU_GRAD;
+}
+__device__ __forceinline__ float aux_grad(int act, float a) {
+  switch (act) {
+    case MDEMI_ACT_GELU_GRAD: return gelu_grad_f(a);
+    case MDEMI_ACT_RELU_GRAD: return a > 0.f ? 1.f : 0.f;
+    default: return silu_grad_f(a);
   }
 }
 

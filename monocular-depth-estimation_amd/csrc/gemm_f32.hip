@@ -314,7 +314,7 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int 
   if (p.bias_mode == MDEMI_BIAS_COL) v += p.bias[j];
   else if (p.bias_mode == MDEMI_BIAS_ROW) v += p.bias[i];
   if (p.pre) p.pre[(int64_t)b * p.pre_bs + (int64_t)i * p.ldpre + j] = v;
-  if (p.act == MDEMI_ACT_GELU_GRAD) v *= gelu_grad_f(p.aux[(int64_t)b * p.aux_bs + (int64_t)i * p.ldaux + j]);
+  if (is_grad_act(p.act)) v *= aux_grad(p.act, p.aux[(int64_t)b * p.aux_bs + (int64_t)i * p.ldaux + j]);
   else if (p.act != MDEMI_ACT_NONE) v = apply_act(p.act, v);
   if (p.res) v += p.res[(int64_t)b * p.res_bs + (int64_t)i * p.ldres + j];
   return v;
@@ -547,6 +547,12 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 #pragma unroll
           MDEMI_EACH v[r] *= gelu_grad_f(buf_ld1(rs, off(p.ldaux, im, in, r)));
         } break;
+        case MDEMI_ACT_RELU_GRAD:
+        case MDEMI_ACT_SILU_GRAD: {
+          const auto rs = make_rsrc(p.aux + (int64_t)b * p.aux_bs + (int64_t)bm * p.ldaux + bn);
+#pragma unroll
+          MDEMI_EACH v[r] *= aux_grad(p.act, buf_ld1(rs, off(p.ldaux, im, in, r)));
+        } break;
         case MDEMI_ACT_NONE: break;
         default: {
 #pragma unroll
@@ -678,7 +684,7 @@ static int validate(const mdemi_gemm_desc* d) {
   if (d->a_layout == MDEMI_L_CONV || d->b_layout == MDEMI_L_CONV) {
     const mdemi_conv_geom& g = d->conv;
     MDEMI_REQUIRE(g.c % 4 == 0, "gemm: conv operand needs C %% 4 == 0 (C=%d)", g.c);
-    MDEMI_REQUIRE(g.kh > 0 && g.kw > 0 && g.stride > 0 && g.pad >= 0 && g.oh > 0 && g.ow > 0,
+    MDEMI_REQUIRE(g.kh > 0 && g.kw > 0 && g.stride > 0 && g.pad > -g.kh && g.pad > -g.kw && g.oh > 0 && g.ow > 0,
                   "gemm: bad conv geometry");
     const int64_t pixels = (int64_t)g.n * g.oh * g.ow;
     const int64_t taps = (int64_t)g.kh * g.kw * g.c;
@@ -699,7 +705,8 @@ static int validate(const mdemi_gemm_desc* d) {
                     d->ldpre < lim, "gemm: leading dimension too large for 32-bit tile offsets");
   if (d->split_k > 1)
     MDEMI_REQUIRE(d->N < lim, "gemm: N too large for split-K slabs");
-  MDEMI_REQUIRE(d->act != MDEMI_ACT_GELU_GRAD || d->aux, "gemm: GELU-grad epilogue needs aux");
+  MDEMI_REQUIRE(!(d->act == MDEMI_ACT_GELU_GRAD || d->act == MDEMI_ACT_RELU_GRAD || d->act == MDEMI_ACT_SILU_GRAD) ||
+                    d->aux, "gemm: *_GRAD epilogue needs aux");
   return MDEMI_OK;
 }
 

@@ -392,7 +392,9 @@ __global__ void copy2d_kernel(const float* __restrict__ src, int64_t sld, float*
 
 extern "C" int mdemi_copy2d(const float* src, int64_t src_ld, float* dst, int64_t dst_ld, int64_t rows, int64_t cols,
                             int32_t accumulate, void* stream) {
-  MDEMI_REQUIRE(src && dst && rows > 0 && cols > 0 && src_ld >= cols && dst_ld >= cols, "copy2d: bad args");
+  // src_ld == 0 broadcasts one source row into every destination row (positional encodings)
+  MDEMI_REQUIRE(src && dst && rows > 0 && cols > 0 && (src_ld >= cols || src_ld == 0) && dst_ld >= cols,
+                "copy2d: bad args");
   const bool v4 = cols % 4 == 0 && src_ld % 4 == 0 && dst_ld % 4 == 0 && ((uintptr_t)src & 15) == 0 &&
                   ((uintptr_t)dst & 15) == 0;
   hipStream_t st = (hipStream_t)stream;

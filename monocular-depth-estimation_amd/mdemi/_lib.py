@@ -20,6 +20,7 @@ import torch  # noqa: F401  (must be imported before the HIP library is mapped)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MDEMI_LIB") or os.path.join(_HERE, "libmdemi.so")  # override: A/B benchmarking
 HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "mdemi.h"))
+HEADER_PATHS = [HEADER_PATH, os.path.abspath(os.path.join(_HERE, "..", "..", "include", "mdemi_ext.h"))]
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 vp = ctypes.c_void_p
@@ -33,6 +34,9 @@ L_KCONTIG, L_MNCONTIG, L_CONV = 0, 1, 2
 OP_NONE, OP_GELU = 0, 1
 BIAS_NONE, BIAS_COL, BIAS_ROW = 0, 1, 2
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_LEAKY, ACT_GELU_GRAD, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
+ACT_SILU, ACT_RELU_GRAD, ACT_SILU_GRAD = 6, 7, 8
+ACT_GRAD_OF = {ACT_GELU: ACT_GELU_GRAD, ACT_RELU: ACT_RELU_GRAD, ACT_SILU: ACT_SILU_GRAD}
+BINS_RELU, BINS_ELU = 0, 1  # include/mdemi_ext.h
 PAD_ZERO, PAD_REPLICATE = 0, 1
 EW_ADD, EW_SIGMOID_SCALE, EW_SIGMOID_SCALE_BWD, EW_AXPBY, EW_ACT_BWD = 0, 1, 2, 3, 4
 
@@ -136,6 +140,29 @@ _SIGS = {
     "mdemi_grad_norm_workspace_size": (sz, [i32]),
     "mdemi_grad_sumsq": (ctypes.c_int, [vp, i32, i64, vp, vp, vp]),
     "mdemi_adamw_step": (ctypes.c_int, [vp, i32, ctypes.POINTER(AdamWGroup), i32, vp, f32, i32, i64, vp, vp]),
+    # ---- include/mdemi_ext.h ----
+    "mdemi_dwconv_fwd": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "mdemi_dwconv_bwd_workspace_size": (sz, [i32, i32, i32, i32, i32]),
+    "mdemi_dwconv_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp,
+                                        vp]),
+    "mdemi_spatial_reduce_workspace_size": (sz, [i32, i64, i32]),
+    "mdemi_spatial_reduce": (ctypes.c_int, [vp, vp, vp, i32, i64, i32, f32, vp, vp]),
+    "mdemi_chan_scale": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, vp]),
+    "mdemi_se_gate_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]),
+    "mdemi_se_gate_bwd_workspace_size": (sz, [i32, i32, i32]),
+    "mdemi_se_gate_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "mdemi_softmax_fwd": (ctypes.c_int, [vp, vp, i64, i32, f32, vp]),
+    "mdemi_softmax_bwd": (ctypes.c_int, [vp, vp, vp, i64, i32, f32, i32, vp]),
+    "mdemi_dropout": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_uint64, ctypes.c_uint64, vp]),
+    "mdemi_binhead_nhwc_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, vp]),
+    "mdemi_binhead_nhwc_bwd_workspace_size": (sz, [i32, i64, i32]),
+    "mdemi_binhead_nhwc_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, vp, vp]),
+    "mdemi_bins_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, f32, f32, vp]),
+    "mdemi_bins_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, vp]),
+    "mdemi_nchw_to_nhwc_pad": (ctypes.c_int, [vp, vp, i32, i32, i64, i32, vp]),
+    "mdemi_pad_fold_replicate": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
+    "mdemi_depth_metrics_workspace_size": (sz, [i32, i32, i32]),
+    "mdemi_depth_metrics": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, f32, i32, vp, vp, vp]),
 }
 
 _lib = None

@@ -48,12 +48,14 @@ def _split_for(M, N, K):
 def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE, b_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
-         res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0, rowsum_a=None):
+         res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0, rowsum_a=None,
+         a_off=0, b_off=0, c_off=0):
+    """a_off/b_off/c_off: element offsets into A/B/C (column slices of wider buffers)."""
     d = L.GemmDesc()
     d.M, d.N, d.K, d.batch = M, N, K, batch
-    d.A, d.lda, d.a_bstride, d.a_layout, d.a_op = A.data_ptr(), lda, a_bstride, a_layout, a_op
-    d.B, d.ldb, d.b_bstride, d.b_layout, d.b_op = B.data_ptr(), ldb, b_bstride, b_layout, b_op
-    d.C, d.ldc, d.c_bstride = C.data_ptr(), ldc, c_bstride
+    d.A, d.lda, d.a_bstride, d.a_layout, d.a_op = A.data_ptr() + 4 * a_off, lda, a_bstride, a_layout, a_op
+    d.B, d.ldb, d.b_bstride, d.b_layout, d.b_op = B.data_ptr() + 4 * b_off, ldb, b_bstride, b_layout, b_op
+    d.C, d.ldc, d.c_bstride = C.data_ptr() + 4 * c_off, ldc, c_bstride
     d.alpha, d.beta = alpha, beta
     d.bias, d.bias_mode, d.act = (bias.data_ptr() if bias is not None else None), bias_mode, act
     d.aux, d.ldaux, d.aux_bstride = (aux.data_ptr() if aux is not None else None), ldaux, aux_bstride
@@ -151,15 +153,19 @@ def linear(x, weight, bias=None, residual=None, in_gelu=False):
 
 
 class _MlpFn(torch.autograd.Function):
-    """fc1 -> GELU -> fc2 (+ residual), Swin/NeW-CRF Mlp (swin_transformer.py:11-29).
+    """fc1 -> act -> [dropout] -> fc2 -> [dropout] (+ residual): Swin/NeW-CRF Mlp
+    (swin_transformer.py:11-29, GELU), Depthformer FeedForwardBlock (feed_forward.py:29-46,
+    SiLU) and nn.TransformerEncoderLayer's feed-forward (layers.py:8, ReLU).
 
-    fc1's epilogue writes both h (pre-activation) and g = gelu(h): HBM is
+    fc1's epilogue writes both h (pre-activation) and g = act(h): HBM is
     plentiful and one extra [rows, 4C] store is far cheaper than recomputing
-    gelu in fc2's operand loader for every N-tile.  Backward: fc2's dgrad
-    epilogue multiplies by gelu'(h) (reading h), so dh never exists unfused."""
+    act in fc2's operand loader for every N-tile.  Backward without dropout:
+    fc2's dgrad epilogue multiplies by act'(h) (reading h), so dh never exists
+    unfused.  Dropout masks are counter hashes regenerated in the backward."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, residual):
+    def forward(ctx, x, w1, b1, w2, b2, residual, cfg):
+        act, p_mid, p_out, seed = cfg
         _require_cuda(x, w1, b1, w2, b2, residual)
         K = x.shape[-1]
         x2 = _c(x).reshape(-1, K)
@@ -168,12 +174,23 @@ class _MlpFn(torch.autograd.Function):
         h = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
         g = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
         gemm(x2, _c(w1), g, M, Hd, K, lda=K, ldb=K, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
-             bias=b1, bias_mode=L.BIAS_COL if b1 is not None else L.BIAS_NONE, act=L.ACT_GELU,
+             bias=b1, bias_mode=L.BIAS_COL if b1 is not None else L.BIAS_NONE, act=act,
              preact=h, ldpre=Hd, split_k=1)
+        if p_mid > 0.0:
+            L.call("mdemi_dropout", g.data_ptr(), g.data_ptr(), g.numel(), float(p_mid), seed, 0, L.stream())
         res2 = _c(residual).reshape(M, N) if residual is not None else None
-        out = linear_fwd_raw(g, _c(w2), b2, residual=res2)
+        if p_out > 0.0:
+            out = linear_fwd_raw(g, _c(w2), b2)
+            L.call("mdemi_dropout", out.data_ptr(), out.data_ptr(), out.numel(), float(p_out), seed + 1, 0,
+                   L.stream())
+            if res2 is not None:
+                L.call("mdemi_elementwise", L.EW_ADD, out.data_ptr(), res2.data_ptr(), out.data_ptr(), out.numel(),
+                       0.0, 0.0, L.stream())
+        else:
+            out = linear_fwd_raw(g, _c(w2), b2, residual=res2)
         ctx.save_for_backward(x2, w1, w2, h, g)
         ctx.flags = (b1 is not None, b2 is not None, residual is not None)
+        ctx.cfg = cfg
         ctx.xshape = x.shape
         return out.view(*x.shape[:-1], N)
 
@@ -181,17 +198,29 @@ class _MlpFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w1, w2, h, g = ctx.saved_tensors
         has_b1, has_b2, has_res = ctx.flags
+        act, p_mid, p_out, seed = ctx.cfg
         M, K = x2.shape
         Hd, N = w1.shape[0], w2.shape[0]
         dy2 = _c(dy).reshape(M, N)
         dev = dy.device
+        if p_out > 0.0:
+            d2 = torch.empty_like(dy2)
+            L.call("mdemi_dropout", dy2.data_ptr(), d2.data_ptr(), d2.numel(), float(p_out), seed + 1, 0, L.stream())
+        else:
+            d2 = dy2
         dw2 = torch.empty(N, Hd, device=dev, dtype=torch.float32)
         db2 = torch.empty(N, device=dev, dtype=torch.float32) if has_b2 else None
-        gemm(dy2, g, dw2, N, Hd, M, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+        gemm(d2, g, dw2, N, Hd, M, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
              rowsum_a=db2)
         dh = torch.empty(M, Hd, device=dev, dtype=torch.float32)
-        gemm(dy2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
-             act=L.ACT_GELU_GRAD, aux=h, ldaux=Hd)
+        if p_mid > 0.0:
+            gemm(d2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
+            L.call("mdemi_dropout", dh.data_ptr(), dh.data_ptr(), dh.numel(), float(p_mid), seed, 0, L.stream())
+            L.call("mdemi_elementwise", L.EW_ACT_BWD, h.data_ptr(), dh.data_ptr(), dh.data_ptr(), dh.numel(),
+                   float(act), 0.0, L.stream())
+        else:
+            gemm(d2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
+                 act=L.ACT_GRAD_OF[act], aux=h, ldaux=Hd)
         del h, g
         dw1 = torch.empty(Hd, K, device=dev, dtype=torch.float32)
         db1 = torch.empty(Hd, device=dev, dtype=torch.float32) if has_b1 else None
@@ -203,12 +232,15 @@ class _MlpFn(torch.autograd.Function):
             gemm(dh, w1, dx, M, K, Hd, lda=Hd, ldb=K, ldc=K, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
             dx = dx.view(ctx.xshape)
         dres = dy if has_res and ctx.needs_input_grad[5] else None
-        return dx, dw1, db1, dw2, db2, dres
+        return dx, dw1, db1, dw2, db2, dres, None
 
 
-def mlp(x, w1, b1, w2, b2, residual=None):
-    """fc2(gelu(fc1(x))) (+ residual) with nn.GELU (exact erf)."""
-    return _MlpFn.apply(x, w1, b1, w2, b2, residual)
+def mlp(x, w1, b1, w2, b2, residual=None, act=L.ACT_GELU, p_mid=0.0, p_out=0.0, training=False):
+    """fc2(dropout(act(fc1(x)))) -> dropout (+ residual); act GELU (exact erf), SiLU or ReLU."""
+    if not training:
+        p_mid = p_out = 0.0
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (p_mid > 0.0 or p_out > 0.0) else 0
+    return _MlpFn.apply(x, w1, b1, w2, b2, residual, (act, float(p_mid), float(p_out), seed))
 
 
 # --------------------------------------------------------------------------
@@ -225,15 +257,18 @@ def _geom(n, h, w, c, oh, ow, kh, kw, stride, pad, pad_mode):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, pad_mode, act):
+    def forward(ctx, x, weight, bias, stride, pad, pad_mode, act, out_hw=None):
         _require_cuda(x, weight, bias)
         x = _c(x)
         n, h, w, c = x.shape
         cout, cin, kh, kw = weight.shape
         if cin != c:
             raise ValueError(f"conv2d: input has {c} channels, weight expects {cin}")
-        oh = (h + 2 * pad - kh) // stride + 1
-        ow = (w + 2 * pad - kw) // stride + 1
+        if out_hw is None:
+            oh = (h + 2 * pad - kh) // stride + 1
+            ow = (w + 2 * pad - kw) // stride + 1
+        else:  # explicit output size: `pad` is the top/left padding (TF 'same', asymmetric)
+            oh, ow = out_hw
         M, K = n * oh * ow, kh * kw * c
         out = torch.empty(n, oh, ow, cout, device=x.device, dtype=torch.float32)
         wf = weight.permute(0, 2, 3, 1).reshape(cout, K).contiguous()
@@ -249,6 +284,7 @@ class _Conv2dFn(torch.autograd.Function):
                  conv=_geom(n, h, w, c, oh, ow, kh, kw, stride, pad, pad_mode))
         ctx.save_for_backward(x, weight, out if act != L.ACT_NONE else None)
         ctx.cfg = (stride, pad, pad_mode, act, bias is not None, pointwise)
+        ctx.explicit = out_hw is not None
         return out
 
     @staticmethod
@@ -274,14 +310,24 @@ class _Conv2dFn(torch.autograd.Function):
                 gemm(dy, weight.reshape(cout, cin), dx, M, c, cout, lda=cout, ldb=cin, ldc=c,
                      a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
             else:
-                if stride != 1 or pad_mode != L.PAD_ZERO:
-                    raise NotImplementedError("conv2d dgrad: stride 1, zero padding only")
+                if stride != 1 or ctx.explicit:
+                    raise NotImplementedError("conv2d dgrad: stride 1 only")
                 # dX = conv(dY, flip(W)^T) with pad k-1-p:  Wd[(ky,kx,co)][c] = W[co][c][k-1-ky][k-1-kx]
                 wd = weight.flip(2, 3).permute(2, 3, 0, 1).reshape(kh * kw * cout, cin).contiguous()
                 dx = torch.empty_like(x)
-                gemm(dy, wd, dx, n * h * w, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
-                     b_layout=L.L_MNCONTIG, split_k=1,
-                     conv=_geom(n, oh, ow, cout, h, w, kh, kw, 1, kh - 1 - pad, L.PAD_ZERO))
+                if pad_mode == L.PAD_ZERO:
+                    gemm(dy, wd, dx, n * h * w, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
+                         b_layout=L.L_MNCONTIG, split_k=1,
+                         conv=_geom(n, oh, ow, cout, h, w, kh, kw, 1, kh - 1 - pad, L.PAD_ZERO))
+                else:
+                    # replicate padding (layer_utils.py:21): gradient of the padded input by a full
+                    # correlation, then fold the border rows/columns onto the edge pixels
+                    hp, wp = h + 2 * pad, w + 2 * pad
+                    dxp = torch.empty(n, hp, wp, c, device=dy.device, dtype=torch.float32)
+                    gemm(dy, wd, dxp, n * hp * wp, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
+                         b_layout=L.L_MNCONTIG, split_k=1,
+                         conv=_geom(n, oh, ow, cout, hp, wp, kh, kw, 1, kh - 1, L.PAD_ZERO))
+                    L.call("mdemi_pad_fold_replicate", dxp.data_ptr(), dx.data_ptr(), n, h, w, c, pad, L.stream())
         want_db = has_bias and ctx.needs_input_grad[2]
         if want_db:
             db = torch.empty(cout, device=dy.device, dtype=torch.float32)
@@ -296,7 +342,7 @@ class _Conv2dFn(torch.autograd.Function):
             dw = dwf.view(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()
         elif want_db:
             colsum(dy.reshape(-1, cout), out=db)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 class _HeadConvFn(torch.autograd.Function):
@@ -331,7 +377,9 @@ class _HeadConvFn(torch.autograd.Function):
         return dx, dw, db
 
 
-def conv2d_nhwc(x, weight, bias=None, stride=1, pad=0, pad_mode=L.PAD_ZERO, act=L.ACT_NONE):
+def conv2d_nhwc(x, weight, bias=None, stride=1, pad=0, pad_mode=L.PAD_ZERO, act=L.ACT_NONE, out_hw=None):
+    if out_hw is not None:
+        return _Conv2dFn.apply(x, weight, bias, stride, pad, pad_mode, act, tuple(out_hw))
     if weight.shape[0] == 1 and stride == 1 and pad_mode == L.PAD_ZERO and act == L.ACT_NONE and \
             2 * pad == weight.shape[-1] - 1 and weight.shape[-1] <= 3 and x.shape[-1] % 4 == 0 and \
             x.shape[-1] <= 128:
@@ -943,3 +991,627 @@ def batch_norm_eval_nhwc(x, weight, bias, running_mean, running_var, eps=1e-5, a
     L.call("mdemi_chnorm_apply", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), running_mean.data_ptr(),
            rstd.data_ptr(), y.data_ptr(), n, hw, c, c, 1, act, L.stream())
     return y
+
+
+# ==========================================================================
+# AdaBins / Depthformer-v8 / EfficientNet-B5 ops (include/mdemi_ext.h)
+# ==========================================================================
+
+
+def _ws(nbytes, device, slot=0):
+    return L.workspace(nbytes, device, slot=slot)
+
+
+class _DWConvFn(torch.autograd.Function):
+    """Depthwise KxK conv, NHWC, no bias; pad_t/pad_l + explicit output size (TF 'same')."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad_t, pad_l, oh, ow):
+        _require_cuda(x, weight)
+        x, weight = _c(x), _c(weight)
+        n, h, w, c = x.shape
+        k = weight.shape[-1]
+        y = torch.empty(n, oh, ow, c, device=x.device, dtype=torch.float32)
+        L.call("mdemi_dwconv_fwd", x.data_ptr(), weight.data_ptr(), y.data_ptr(), n, h, w, c, k, stride, pad_t, pad_l,
+               oh, ow, L.stream())
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (stride, pad_t, pad_l, oh, ow)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        stride, pad_t, pad_l, oh, ow = ctx.cfg
+        dy = _c(dy)
+        n, h, w, c = x.shape
+        k = weight.shape[-1]
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(weight) if ctx.needs_input_grad[1] else None
+        lib = L.load()
+        ws = _ws(lib.mdemi_dwconv_bwd_workspace_size(n, c, k, oh, ow), x.device)
+        L.check(lib.mdemi_dwconv_bwd(dy.data_ptr(), x.data_ptr(), weight.data_ptr(), L.ptr(dx), L.ptr(dw), n, h, w, c,
+                                     k, stride, pad_t, pad_l, oh, ow, ws.data_ptr(), L.stream()), "dwconv_bwd")
+        return dx, dw, None, None, None, None, None
+
+
+def same_pad(size, k, s):
+    """TF 'same' padding (gen-efficientnet Conv2dSame): output ceil(size/s), extra pad at the end."""
+    out = -(-size // s)
+    total = max((out - 1) * s + k - size, 0)
+    return out, total // 2
+
+
+def dwconv_nhwc(x, weight, stride=1, same=True, pad=None):
+    n, h, w, c = x.shape
+    k = weight.shape[-1]
+    if same:
+        oh, pt = same_pad(h, k, stride)
+        ow, pl = same_pad(w, k, stride)
+    else:
+        pt = pl = k // 2 if pad is None else pad
+        oh = (h + 2 * pt - k) // stride + 1
+        ow = (w + 2 * pl - k) // stride + 1
+    return _DWConvFn.apply(x, weight, stride, pt, pl, oh, ow)
+
+
+def spatial_reduce(a, b=None, scale=1.0):
+    """out[n, c] = scale * sum_p a[n, p, c] * b[n, p, c]  (NHWC or [N, P, C]); no autograd."""
+    n, c = a.shape[0], a.shape[-1]
+    hw = a[0].numel() // c
+    out = torch.empty(n, c, device=a.device, dtype=torch.float32)
+    lib = L.load()
+    ws = _ws(lib.mdemi_spatial_reduce_workspace_size(n, hw, c), a.device, slot=3)
+    L.check(lib.mdemi_spatial_reduce(a.data_ptr(), L.ptr(b), out.data_ptr(), n, hw, c, float(scale), ws.data_ptr(),
+                                     L.stream()), "spatial_reduce")
+    return out
+
+
+def _chan_scale(x, g, add=None):
+    y = torch.empty_like(x)
+    n, c = x.shape[0], x.shape[-1]
+    L.call("mdemi_chan_scale", x.data_ptr(), g.data_ptr(), L.ptr(add), y.data_ptr(), n, x[0].numel() // c, c,
+           L.stream())
+    return y
+
+
+class _SpatialMeanFn(torch.autograd.Function):
+    """mean over the spatial / token axis of an NHWC or [N, P, C] tensor -> [N, C]."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _require_cuda(x)
+        x = _c(x)
+        hw = x[0].numel() // x.shape[-1]
+        ctx.shape = x.shape
+        ctx.hw = hw
+        return spatial_reduce(x, None, 1.0 / hw)
+
+    @staticmethod
+    def backward(ctx, dy):
+        zeros = torch.zeros(ctx.shape, device=dy.device, dtype=torch.float32)
+        return _chan_scale(zeros, torch.zeros_like(dy), _scale(_c(dy), 1.0 / ctx.hw))
+
+
+def spatial_mean(x):
+    return _SpatialMeanFn.apply(x)
+
+
+class _SqueezeExciteFn(torch.autograd.Function):
+    """EfficientNet SqueezeExcite: x * sigmoid(W_e swish(W_r mean(x) + b_r) + b_e), NHWC."""
+
+    @staticmethod
+    def forward(ctx, x, wr, br, we, be):
+        _require_cuda(x, wr, br, we, be)
+        x = _c(x)
+        n, c = x.shape[0], x.shape[-1]
+        hw = x[0].numel() // c
+        r = wr.shape[0]
+        pooled = spatial_reduce(x, None, 1.0 / hw)
+        hid = torch.empty(n, r, device=x.device, dtype=torch.float32)
+        gate = torch.empty(n, c, device=x.device, dtype=torch.float32)
+        L.call("mdemi_se_gate_fwd", pooled.data_ptr(), _c(wr).data_ptr(), br.data_ptr(), _c(we).data_ptr(),
+               be.data_ptr(), hid.data_ptr(), gate.data_ptr(), n, c, r, L.stream())
+        y = _chan_scale(x, gate)
+        ctx.save_for_backward(x, wr, we, pooled, hid, gate)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wr, we, pooled, hid, gate = ctx.saved_tensors
+        dy = _c(dy)
+        n, c = x.shape[0], x.shape[-1]
+        hw = x[0].numel() // c
+        r = wr.shape[0]
+        dgate = spatial_reduce(dy, x, 1.0)
+        dpooled = torch.empty(n, c, device=x.device, dtype=torch.float32)
+        dwr, dbr = torch.empty_like(wr), torch.empty(r, device=x.device, dtype=torch.float32)
+        dwe, dbe = torch.empty_like(we), torch.empty(c, device=x.device, dtype=torch.float32)
+        lib = L.load()
+        ws = _ws(lib.mdemi_se_gate_bwd_workspace_size(n, c, r), x.device, slot=3)
+        L.check(lib.mdemi_se_gate_bwd(pooled.data_ptr(), _c(wr).data_ptr(), _c(we).data_ptr(), hid.data_ptr(),
+                                      gate.data_ptr(), dgate.data_ptr(), dpooled.data_ptr(), dwr.data_ptr(),
+                                      dbr.data_ptr(), dwe.data_ptr(), dbe.data_ptr(), n, c, r, ws.data_ptr(),
+                                      L.stream()), "se_gate_bwd")
+        # d/dx of x * gate plus the pooling path: dpooled / HW broadcast over positions
+        dx = _chan_scale(dy, gate, _scale(dpooled, 1.0 / hw))
+        return dx, dwr, dbr, dwe, dbe
+
+
+def _scale(t, s):
+    out = torch.empty_like(t)
+    L.call("mdemi_elementwise", L.EW_AXPBY, t.data_ptr(), t.data_ptr(), out.data_ptr(), t.numel(), float(s), 0.0,
+           L.stream())
+    return out
+
+
+def squeeze_excite(x, wr, br, we, be):
+    """wr [R, C], we [C, R] (the 1x1 conv weights flattened)."""
+    return _SqueezeExciteFn.apply(x, wr, br, we, be)
+
+
+class _SoftmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, scale):
+        _require_cuda(x)
+        x = _c(x)
+        cols = x.shape[-1]
+        y = torch.empty_like(x)
+        L.call("mdemi_softmax_fwd", x.data_ptr(), y.data_ptr(), x.numel() // cols, cols, float(scale), L.stream())
+        ctx.save_for_backward(y)
+        ctx.scale = scale
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = _c(dy)
+        cols = y.shape[-1]
+        dx = torch.empty_like(y)
+        L.call("mdemi_softmax_bwd", y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // cols, cols,
+               float(ctx.scale), 0, L.stream())
+        return dx, None
+
+
+def softmax_lastdim(x, scale=1.0):
+    """softmax(scale * x, dim=-1)."""
+    return _SoftmaxFn.apply(x, scale)
+
+
+_drop_counter = [0]
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed, offset):
+        _require_cuda(x)
+        x = _c(x)
+        y = torch.empty_like(x)
+        L.call("mdemi_dropout", x.data_ptr(), y.data_ptr(), x.numel(), float(p), seed, offset, L.stream())
+        ctx.cfg = (p, seed, offset)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, seed, offset = ctx.cfg
+        dy = _c(dy)
+        dx = torch.empty_like(dy)
+        L.call("mdemi_dropout", dy.data_ptr(), dx.data_ptr(), dy.numel(), float(p), seed, offset, L.stream())
+        return dx, None, None, None
+
+
+def dropout(x, p, training):
+    """Inverted dropout; the mask is a hash of (seed, element index), drawn from torch's CPU generator
+    once per call, so the backward regenerates it instead of storing it."""
+    if not training or p == 0.0:
+        return x
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    off = _drop_counter[0]
+    _drop_counter[0] += x.numel()
+    return _DropoutFn.apply(x, p, seed, off)
+
+
+class _BinHeadNHWCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, centers):
+        _require_cuda(logits, centers)
+        logits, centers = _c(logits), _c(centers)
+        b, k = logits.shape[0], logits.shape[-1]
+        hw = logits[0].numel() // k
+        pred = torch.empty(b, hw, device=logits.device, dtype=torch.float32)
+        stats = torch.empty(b, hw, 2, device=logits.device, dtype=torch.float32)
+        L.call("mdemi_binhead_nhwc_fwd", logits.data_ptr(), centers.data_ptr(), pred.data_ptr(), stats.data_ptr(), b,
+               hw, k, L.stream())
+        ctx.save_for_backward(logits, centers, pred, stats)
+        return pred
+
+    @staticmethod
+    def backward(ctx, dpred):
+        logits, centers, pred, stats = ctx.saved_tensors
+        dpred = _c(dpred)
+        b, k = logits.shape[0], logits.shape[-1]
+        hw = logits[0].numel() // k
+        dlogits = torch.empty_like(logits)
+        dcenters = torch.empty(b, k, device=logits.device, dtype=torch.float32)
+        lib = L.load()
+        ws = _ws(lib.mdemi_binhead_nhwc_bwd_workspace_size(b, hw, k), logits.device)
+        L.check(lib.mdemi_binhead_nhwc_bwd(logits.data_ptr(), centers.data_ptr(), pred.data_ptr(), stats.data_ptr(),
+                                           dpred.data_ptr(), dlogits.data_ptr(), dcenters.data_ptr(), b, hw, k,
+                                           ws.data_ptr(), L.stream()), "binhead_nhwc_bwd")
+        return dlogits, dcenters.view_as(centers)
+
+
+def bin_head_nhwc(logits, centers):
+    """logits [B, H, W, K] (channels-last) -> pred [B, 1, H, W] = sum_k softmax(logits)_k * centers[b, k]."""
+    b, h, w, k = logits.shape
+    return _BinHeadNHWCFn.apply(logits, centers.reshape(b, k)).view(b, 1, h, w)
+
+
+class _BinsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, raw, mode, min_val, max_val):
+        _require_cuda(raw)
+        raw = _c(raw)
+        b, k = raw.shape
+        widths = torch.empty(b, k, device=raw.device, dtype=torch.float32)
+        edges = torch.empty(b, k + 1, device=raw.device, dtype=torch.float32)
+        centers = torch.empty(b, k, device=raw.device, dtype=torch.float32)
+        L.call("mdemi_bins_fwd", raw.data_ptr(), widths.data_ptr(), edges.data_ptr(), centers.data_ptr(), b, k,
+               mode, float(min_val), float(max_val), L.stream())
+        ctx.save_for_backward(raw)
+        ctx.cfg = (mode, min_val, max_val)
+        return widths, edges, centers
+
+    @staticmethod
+    def backward(ctx, dwidths, dedges, dcenters):
+        (raw,) = ctx.saved_tensors
+        mode, min_val, max_val = ctx.cfg
+        b, k = raw.shape
+        dc = _c(dcenters) if dcenters is not None else torch.zeros(b, k, device=raw.device, dtype=torch.float32)
+        draw = torch.empty_like(raw)
+        L.call("mdemi_bins_bwd", raw.data_ptr(), dc.data_ptr(), L.ptr(_c(dedges) if dedges is not None else None),
+               L.ptr(_c(dwidths) if dwidths is not None else None), draw.data_ptr(), b, k, mode, float(min_val),
+               float(max_val), L.stream())
+        return draw, None, None, None
+
+
+def bins_from_raw(raw, mode, min_val, max_val, with_widths=False):
+    """Regressor output [B, K] -> (bin_edges [B, K+1], centers [B, K]) (and the normalised widths
+    first when with_widths).  mode: L.BINS_RELU (AdaBins norm='linear') or L.BINS_ELU
+    (Depthformer v8)."""
+    w, e, c = _BinsFn.apply(raw, mode, min_val, max_val)
+    return (w, e, c) if with_widths else (e, c)
+
+
+def nchw_to_nhwc_pad(x, cp):
+    """Image NCHW -> NHWC with channels zero-padded to cp (no autograd: the image is an input)."""
+    _require_cuda(x)
+    x = _c(x)
+    n, c, h, w = x.shape
+    y = torch.empty(n, h, w, cp, device=x.device, dtype=torch.float32)
+    L.call("mdemi_nchw_to_nhwc_pad", x.data_ptr(), y.data_ptr(), n, c, h * w, cp, L.stream())
+    return y
+
+
+def depth_metrics(pred, gt, rect, min_depth, max_depth, clamp_pred=True):
+    """Per-image [a1, a2, a3, abs_rel, sq_rel, rmse, rmse_log, silog, log_10, n_valid] (fp64) over
+    crop rect (y0, y1, x0, x1) & min_depth < gt < max_depth (utils/depth_utils.py:4-54)."""
+    _require_cuda(pred, gt)
+    pred, gt = _c(pred), _c(gt)
+    b = pred.shape[0]
+    h, w = pred.shape[-2:]
+    out = torch.empty(b, 10, device=pred.device, dtype=torch.float64)
+    lib = L.load()
+    ws = _ws(lib.mdemi_depth_metrics_workspace_size(b, h, w), pred.device, slot=3)
+    y0, y1, x0, x1 = rect
+    L.check(lib.mdemi_depth_metrics(pred.data_ptr(), gt.data_ptr(), b, h, w, y0, y1, x0, x1, float(min_depth),
+                                    float(max_depth), int(clamp_pred), out.data_ptr(), ws.data_ptr(), L.stream()),
+            "depth_metrics")
+    return out
+
+
+class _AttentionFn(torch.autograd.Function):
+    """Multi-head scaled dot-product attention over column slices of token-major buffers
+    ([B*S, ld] rows): per head h, P = softmax(scale * Q_h K_h^T) (returned, [B, heads, Sq, Sk]),
+    O_h = dropout(P) V_h written to out[:, h*dv:(h+1)*dv].  QK^T / PV / their gradients are
+    batched MFMA GEMMs (batch = B); softmax and dropout are row sweeps.  Serves
+    nn.TransformerEncoderLayer's self-attention (layers.py:8), PreNormLunaBlock's two
+    attentions (luna_layer.py:202-250) and SelfAttentionBlock (self_attention.py:61-80)."""
+
+    @staticmethod
+    def forward(ctx, qsrc, ksrc, vsrc, cfg):
+        B, Sq, Sk, heads, dqk, dv, q_off, k_off, v_off, scale, p, seed = cfg
+        _require_cuda(qsrc, ksrc, vsrc)
+        ldq, ldk, ldv = qsrc.shape[-1], ksrc.shape[-1], vsrc.shape[-1]
+        dev = qsrc.device
+        P = torch.empty(B, heads, Sq, Sk, device=dev, dtype=torch.float32)
+        hs = Sq * Sk
+        for h in range(heads):
+            gemm(qsrc, ksrc, P, Sq, Sk, dqk, lda=ldq, ldb=ldk, ldc=Sk, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+                 batch=B, a_bstride=Sq * ldq, b_bstride=Sk * ldk, c_bstride=heads * hs, a_off=q_off + h * dqk,
+                 b_off=k_off + h * dqk, c_off=h * hs)
+        L.call("mdemi_softmax_fwd", P.data_ptr(), P.data_ptr(), B * heads * Sq, Sk, float(scale), L.stream())
+        Pd = P
+        if p > 0.0:
+            Pd = torch.empty_like(P)
+            L.call("mdemi_dropout", P.data_ptr(), Pd.data_ptr(), P.numel(), float(p), seed, 0, L.stream())
+        out = torch.empty(B * Sq, heads * dv, device=dev, dtype=torch.float32)
+        for h in range(heads):
+            gemm(Pd, vsrc, out, Sq, dv, Sk, lda=Sk, ldb=ldv, ldc=heads * dv, a_layout=L.L_KCONTIG,
+                 b_layout=L.L_MNCONTIG, batch=B, a_bstride=heads * hs, b_bstride=Sk * ldv, c_bstride=Sq * heads * dv,
+                 a_off=h * hs, b_off=v_off + h * dv, c_off=h * dv)
+        ctx.save_for_backward(qsrc, ksrc, vsrc, P)
+        ctx.cfg = cfg
+        return out, P
+
+    @staticmethod
+    def backward(ctx, dout, dP_ext):
+        qsrc, ksrc, vsrc, P = ctx.saved_tensors
+        B, Sq, Sk, heads, dqk, dv, q_off, k_off, v_off, scale, p, seed = ctx.cfg
+        ldq, ldk, ldv = qsrc.shape[-1], ksrc.shape[-1], vsrc.shape[-1]
+        hs = Sq * Sk
+        Pd = P
+        if p > 0.0:
+            Pd = torch.empty_like(P)
+            L.call("mdemi_dropout", P.data_ptr(), Pd.data_ptr(), P.numel(), float(p), seed, 0, L.stream())
+        # one gradient buffer per distinct source tensor; columns outside the used slices are zero
+        bufs, spans = {}, {}
+        for t, off, width in ((qsrc, q_off, heads * dqk), (ksrc, k_off, heads * dqk), (vsrc, v_off, heads * dv)):
+            spans.setdefault(id(t), []).append((off, width))
+        for t in (qsrc, ksrc, vsrc):
+            if id(t) in bufs:
+                continue
+            covered = sum(w for _, w in spans[id(t)])
+            full = covered == t.shape[-1] and dout is not None
+            bufs[id(t)] = torch.empty_like(t) if full else torch.zeros_like(t)
+        dq, dk, dvv = bufs[id(qsrc)], bufs[id(ksrc)], bufs[id(vsrc)]
+        dP = torch.empty_like(P)
+        if dout is not None:
+            dout = _c(dout)
+            for h in range(heads):
+                gemm(dout, vsrc, dP, Sq, Sk, dv, lda=heads * dv, ldb=ldv, ldc=Sk, a_layout=L.L_KCONTIG,
+                     b_layout=L.L_KCONTIG, batch=B, a_bstride=Sq * heads * dv, b_bstride=Sk * ldv,
+                     c_bstride=heads * hs, a_off=h * dv, b_off=v_off + h * dv, c_off=h * hs)
+                gemm(Pd, dout, dvv, Sk, dv, Sq, lda=Sk, ldb=heads * dv, ldc=ldv, a_layout=L.L_MNCONTIG,
+                     b_layout=L.L_MNCONTIG, batch=B, a_bstride=heads * hs, b_bstride=Sq * heads * dv,
+                     c_bstride=Sk * ldv, a_off=h * hs, b_off=h * dv, c_off=v_off + h * dv)
+            if p > 0.0:
+                L.call("mdemi_dropout", dP.data_ptr(), dP.data_ptr(), dP.numel(), float(p), seed, 0, L.stream())
+            if dP_ext is not None:
+                dP_ext = _c(dP_ext)
+                L.call("mdemi_elementwise", L.EW_ADD, dP.data_ptr(), dP_ext.data_ptr(), dP.data_ptr(), dP.numel(),
+                       0.0, 0.0, L.stream())
+        elif dP_ext is not None:  # only the returned probabilities carry a gradient
+            _copy2d(_c(dP_ext).view(-1, Sk), dP.view(-1, Sk))
+        else:
+            dP.zero_()
+        L.call("mdemi_softmax_bwd", P.data_ptr(), dP.data_ptr(), dP.data_ptr(), B * heads * Sq, Sk, float(scale), 0,
+               L.stream())
+        for h in range(heads):
+            gemm(dP, ksrc, dq, Sq, dqk, Sk, lda=Sk, ldb=ldk, ldc=ldq, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
+                 batch=B, a_bstride=heads * hs, b_bstride=Sk * ldk, c_bstride=Sq * ldq, a_off=h * hs,
+                 b_off=k_off + h * dqk, c_off=q_off + h * dqk)
+            gemm(dP, qsrc, dk, Sk, dqk, Sq, lda=Sk, ldb=ldq, ldc=ldk, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+                 batch=B, a_bstride=heads * hs, b_bstride=Sq * ldq, c_bstride=Sk * ldk, a_off=h * hs,
+                 b_off=q_off + h * dqk, c_off=k_off + h * dqk)
+        seen, grads = set(), []
+        for t, g in ((qsrc, dq), (ksrc, dk), (vsrc, dvv)):
+            grads.append(None if id(t) in seen else g)
+            seen.add(id(t))
+        return grads[0], grads[1], grads[2], None
+
+
+def attention(qsrc, ksrc, vsrc, B, Sq, Sk, heads, dqk, dv, scale, q_off=0, k_off=0, v_off=0, p=0.0,
+              training=False):
+    """Returns (out [B*Sq, heads*dv], probs [B, heads, Sq, Sk]).  q/k/v are column slices
+    (offsets q_off/k_off/v_off, head-major) of 2-D token-major buffers [B*S, ld]; a buffer may
+    feed several of them (e.g. a fused qkv projection)."""
+    p = float(p) if training else 0.0
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0.0 else 0
+    cfg = (B, Sq, Sk, heads, dqk, dv, q_off, k_off, v_off, float(scale), p, seed)
+    return _AttentionFn.apply(_c(qsrc), _c(ksrc), _c(vsrc), cfg)
+
+
+def _bgemm_raw(A, B, ta, tb, bias=None):
+    """C[b] = op(A[b]) @ op(B[b]) (+ bias[j]); A/B dense [nb, r, c] or [r, c] / [1, r, c] (shared)."""
+    nb = max(A.shape[0] if A.dim() == 3 else 1, B.shape[0] if B.dim() == 3 else 1)
+    ar, ac = A.shape[-2:]
+    br, bc = B.shape[-2:]
+    M, K = (ac, ar) if ta else (ar, ac)
+    K2, N = (bc, br) if tb else (br, bc)
+    if K != K2:
+        raise ValueError(f"bgemm: inner sizes differ ({K} vs {K2})")
+    C = torch.empty(nb, M, N, device=A.device, dtype=torch.float32)
+    a_bs = ar * ac if (A.dim() == 3 and A.shape[0] > 1) else 0
+    b_bs = br * bc if (B.dim() == 3 and B.shape[0] > 1) else 0
+    gemm(A, B, C, M, N, K, lda=ac, ldb=bc, ldc=N, a_layout=L.L_MNCONTIG if ta else L.L_KCONTIG,
+         b_layout=L.L_KCONTIG if tb else L.L_MNCONTIG, batch=nb, a_bstride=a_bs, b_bstride=b_bs,
+         c_bstride=M * N, bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE)
+    return C
+
+
+class _BatchedGemmFn(torch.autograd.Function):
+    """C[b] = op(A[b]) @ op(B[b]) (+ bias[j]), op = transpose when flagged; A or B may be shared
+    by every batch entry (stored once).  Serves PixelWiseDotProduct (layers.py:38-43) and the
+    conv_out-folded bin logits of AdaBins (unet_adaptive_bins.py:88-97)."""
+
+    @staticmethod
+    def forward(ctx, A, B, bias, ta, tb):
+        _require_cuda(A, B, bias)
+        A, B = _c(A), _c(B)
+        C = _bgemm_raw(A, B, ta, tb, bias)
+        ctx.save_for_backward(A, B)
+        shared_a = not (A.dim() == 3 and A.shape[0] > 1)
+        shared_b = not (B.dim() == 3 and B.shape[0] > 1)
+        ctx.cfg = (ta, tb, C.shape[0], shared_a, shared_b, bias is not None)
+        return C
+
+    @staticmethod
+    def backward(ctx, dC):
+        A, B = ctx.saved_tensors
+        ta, tb, nb, shared_a, shared_b, has_bias = ctx.cfg
+        dC = _c(dC)
+
+        def run(X, tx, Y, ty, shared):
+            out = _bgemm_raw(X, Y, tx, ty)
+            if shared and nb > 1:  # sum the per-entry gradients of a shared operand
+                red = torch.empty(out.shape[1:], device=out.device, dtype=torch.float32)
+                colsum(out.view(nb, -1), out=red.view(-1))
+                return red
+            return out
+
+        dA = dB = db = None
+        if ctx.needs_input_grad[0]:
+            # not ta: dA = dC op(B)^T ; ta: dA = op(B) dC^T
+            dA = run(dC, False, B, not tb, shared_a) if not ta else run(B, tb, dC, True, shared_a)
+            dA = dA.view_as(A)
+        if ctx.needs_input_grad[1]:
+            # not tb: dB = op(A)^T dC ; tb: dB = dC^T op(A)
+            dB = run(A, not ta, dC, False, shared_b) if not tb else run(dC, True, A, ta, shared_b)
+            dB = dB.view_as(B)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = colsum(dC.view(-1, dC.shape[-1]))
+        return dA, dB, db, None, None
+
+
+def bgemm(A, B, bias=None, ta=False, tb=False):
+    """Batched op(A) @ op(B) on MFMA tiles; A/B are [nb, r, c] or [r, c] (shared over the batch)."""
+    return _BatchedGemmFn.apply(A, B, bias, ta, tb)
+
+
+class _UpConcatFn(torch.autograd.Function):
+    """cat([resize(x), skip], channels) (unet_adaptive_bins.py:22-23) or cat([skip, resize(x)])
+    (layer_utils.py:114-120): the bilinear sweep writes straight into its channel slice."""
+
+    @staticmethod
+    def forward(ctx, x, skip, oh, ow, align, sh, sw, x_first):
+        _require_cuda(x, skip)
+        x, skip = _c(x), _c(skip)
+        n, h, w, cx = x.shape
+        cs = skip.shape[-1]
+        out = torch.empty(n, oh, ow, cx + cs, device=x.device, dtype=torch.float32)
+        ct = cx + cs
+        xo, so = (0, cx) if x_first else (cs, 0)
+        L.call("mdemi_bilinear_fwd", x.data_ptr(), out.data_ptr() + 4 * xo, n, h, w, cx, oh, ow, int(align), float(sh),
+               float(sw), cx, ct, L.stream())
+        _copy2d(skip.view(-1, cs), out.view(-1, ct)[:, so:so + cs])
+        ctx.cfg = (n, h, w, cx, cs, oh, ow, align, sh, sw, xo, so)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, cx, cs, oh, ow, align, sh, sw, xo, so = ctx.cfg
+        dy = _c(dy)
+        ct = cx + cs
+        dx = torch.empty(n, h, w, cx, device=dy.device, dtype=torch.float32)
+        L.call("mdemi_bilinear_bwd", dy.data_ptr() + 4 * xo, dx.data_ptr(), n, h, w, cx, oh, ow, int(align), float(sh),
+               float(sw), ct, cx, 0, L.stream())
+        ds = torch.empty(n, oh, ow, cs, device=dy.device, dtype=torch.float32)
+        _copy2d(dy.view(-1, ct)[:, so:so + cs], ds.view(-1, cs))
+        return dx, ds, None, None, None, None, None, None
+
+
+def upsample_concat(x, skip, size=None, scale_factor=None, align_corners=True, x_first=True):
+    n, h, w, c = x.shape
+    if size is not None:
+        oh, ow = size
+        sh = sw = 0.0
+    else:
+        oh, ow = int(math.floor(h * scale_factor)), int(math.floor(w * scale_factor))
+        sh = sw = 0.0 if align_corners else float(scale_factor)
+    return _UpConcatFn.apply(x, skip, oh, ow, align_corners, sh, sw, x_first)
+
+
+class _LinearActFn(torch.autograd.Function):
+    """act(x W^T + b) with the activation in the GEMM epilogue (pre-activation kept for the
+    backward): nn.Sequential(Linear, LeakyReLU/SiLU) stacks (miniViT.py:19-23,
+    decoder_v8.py:82-90)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, act):
+        _require_cuda(x, weight, bias)
+        K = x.shape[-1]
+        x2 = _c(x).reshape(-1, K)
+        M, N = x2.shape[0], weight.shape[0]
+        out = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        pre = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        gemm(x2, _c(weight), out, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+             bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act, preact=pre, ldpre=N,
+             split_k=1)
+        ctx.save_for_backward(x2, weight, pre)
+        ctx.act = act
+        ctx.has_bias = bias is not None
+        ctx.xshape = x.shape
+        return out.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, pre = ctx.saved_tensors
+        dy2 = _c(dy).reshape(pre.shape)
+        dpre = torch.empty_like(pre)
+        L.call("mdemi_elementwise", L.EW_ACT_BWD, pre.data_ptr(), dy2.data_ptr(), dpre.data_ptr(), pre.numel(),
+               float(ctx.act), 0.0, L.stream())
+        M, K = x2.shape
+        N = weight.shape[0]
+        dx = torch.empty(M, K, device=dy.device, dtype=torch.float32)
+        gemm(dpre, weight, dx, M, K, N, lda=N, ldb=K, ldc=K, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
+        dw = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+        db = torch.empty(N, device=dy.device, dtype=torch.float32) if ctx.has_bias else None
+        gemm(dpre, x2, dw, N, K, M, lda=N, ldb=K, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG, rowsum_a=db)
+        return dx.view(ctx.xshape), dw, db, None
+
+
+def linear_act(x, weight, bias, act):
+    return _LinearActFn.apply(x, weight, bias, act)
+
+
+class _RowsFn(torch.autograd.Function):
+    """x[b, start:start+count, :] for every b of a [B, S, C] tensor, as a dense [B, count, C]."""
+
+    @staticmethod
+    def forward(ctx, x, start, count):
+        _require_cuda(x)
+        x = _c(x)
+        B, S, C = x.shape
+        out = torch.empty(B, count, C, device=x.device, dtype=torch.float32)
+        src = x.view(B, S * C)[:, start * C:(start + count) * C]
+        _copy2d(src, out.view(B, count * C))
+        ctx.cfg = (B, S, C, start, count)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, S, C, start, count = ctx.cfg
+        dx = torch.zeros(B, S, C, device=dy.device, dtype=torch.float32)
+        _copy2d(_c(dy).view(B, count * C), dx.view(B, S * C)[:, start * C:(start + count) * C])
+        return dx, None, None
+
+
+def take_rows(x, start, count):
+    return _RowsFn.apply(x, start, count)
+
+
+class _AddRowsBroadcastFn(torch.autograd.Function):
+    """y[b] = x[b] + t[:S] for x [B, S, C]: the learned positional encodings (layers.py:26)."""
+
+    @staticmethod
+    def forward(ctx, x, table):
+        _require_cuda(x, table)
+        x = _c(x)
+        B, S, C = x.shape
+        y = torch.empty_like(x)
+        _copy2d(x.view(B, S * C), y.view(B, S * C))
+        L.call("mdemi_copy2d", _c(table).data_ptr(), 0, y.data_ptr(), S * C, B, S * C, 1, L.stream())
+        ctx.cfg = (B, S, C, table.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, S, C, tshape = ctx.cfg
+        dy = _c(dy)
+        dt = torch.zeros(tshape, device=dy.device, dtype=torch.float32)
+        colsum(dy.view(B, S * C), out=dt.view(-1)[:S * C])
+        return dy, dt
+
+
+def add_rows_broadcast(x, table):
+    return _AddRowsBroadcastFn.apply(x, table)

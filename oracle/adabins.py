@@ -98,3 +98,11 @@ def adabins_head(P, features, min_val=1e-3, max_val=10.0):  # unet_adaptive_bins
     widths, range_maps = mvit(P, "adaptive_bins_layer.", unet_out)
     probs = torch.softmax(F.conv2d(range_maps, P["conv_out.0.weight"], P["conv_out.0.bias"]), dim=1)
     return bins_to_pred(probs, widths, min_val, max_val)
+
+
+def unet_adaptive_bins(P, x, min_val=1e-3, max_val=10.0):
+    """Whole UnetAdaptiveBins.forward (unet_adaptive_bins.py:93-109) with the restated
+    EfficientNet-B5 encoder (oracle/efficientnet.py — parity unpinned)."""
+    from . import efficientnet as oeff
+    feats = oeff.features(P, "encoder.original_model.", x, last=11)
+    return adabins_head(P, feats, min_val, max_val)

@@ -146,3 +146,113 @@ def test_newcrfs_tiny07_end_to_end():
     m = NewCRFDepth(version="tiny07", max_depth=10.0, drop_path_rate=0.0)
     n = run_case(g, m, lambda m, i: m(i["img"]), ["depth"], {}, {}, no_input_grad=("img",))
     assert n == len(list(m.parameters()))
+
+
+# ---------------------------------------------------------------------------
+# AdaBins (model/Adabins) — EfficientNet-B5 features stand in as stored maps
+# ---------------------------------------------------------------------------
+class _Const(torch.nn.Module):
+    def __init__(self, holder, idx):
+        super().__init__()
+        self.__dict__["_holder"] = holder
+        self.idx = idx
+
+    def forward(self, x):
+        return self._holder[self.idx]
+
+
+def fake_backend(holder):
+    """Module tree walked like gen-efficientnet's; feature k returns holder[k] (NHWC)."""
+    m = torch.nn.Module()
+    m.conv_stem, m.bn1, m.act1 = _Const(holder, 1), _Const(holder, 2), _Const(holder, 3)
+    m.blocks = torch.nn.Sequential(*[_Const(holder, 4 + i) for i in range(7)])
+    m.conv_head, m.act2 = _Const(holder, 11), _Const(holder, 12)
+    return m
+
+
+def test_adabins_head():
+    """UnetAdaptiveBins after the encoder (decoder, mViT, folded conv_out + bin head) vs the reference."""
+    from mdemi.model.Adabins import UnetAdaptiveBins
+    g = Golden("adabins_head")
+    holder = {}
+    m = UnetAdaptiveBins(fake_backend(holder), n_bins=256, min_val=1e-3, max_val=10.0)
+
+    def fwd(m, i):
+        holder.clear()
+        for k, v in i.items():
+            holder[int(k[1:])] = v
+        return m(torch.zeros(1, 3, 8, 8, device=DEV))
+
+    n = run_case(g, m, fwd, ["pred", "bin_edges"], {}, {k: "nchw" for k in g.input_names()})
+    assert n == len(list(m.parameters()))
+
+
+def test_mvit():
+    from mdemi.model.Adabins import mViT
+    g = Golden("mvit")
+    m = mViT(128, n_query_channels=128, patch_size=16, dim_out=256, embedding_dim=128, norm="linear")
+    n = run_case(g, m, lambda m, i: m(i["x"]), ["bin_widths", "range_maps"], {"range_maps": "nchw"},
+                 {"x": "nchw"})
+    assert n == len(list(m.parameters()))
+
+
+def _oracle_params(model, seed, scale):
+    from oracle.weights import closed_form_fill
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    closed_form_fill(sd, seed=seed, scale=scale)
+    model.load_state_dict(sd)
+    return {k: (v.double().requires_grad_(True) if torch.is_floating_point(v) else v) for k, v in sd.items()}
+
+
+def test_efficientnet_b5_encoder_vs_oracle():
+    """Restated tf_efficientnet_b5_ap (parity unpinned: third-party, not offline) — libmdemi vs the
+    CPU oracle restatement on the same closed-form weights: features [4,5,6,8,11] and all grads."""
+    from mdemi.model.gen_efficientnet import tf_efficientnet_b5_ap, walk_features
+    from oracle import efficientnet as oeff
+    from oracle.weights import rng_array
+    net = tf_efficientnet_b5_ap()
+    del net.bn2, net.global_pool, net.classifier
+    P = _oracle_params(net, 0.31, 0.05)
+    net = net.to(DEV).train()
+    img = torch.from_numpy(rng_array((2, 3, 64, 96), 77))
+    fg = walk_features(net, img.float().to(DEV), 11)
+    fr = oeff.features(P, "", img.double(), 11)
+    loss_g, loss_r = 0, 0
+    for k in (4, 5, 6, 8, 11):
+        a, r = fg[k], fr[k]
+        err = (nhwc_to_nchw(a).double().cpu() - r).abs().max().item()
+        assert err <= 1e-4 * r.abs().max().item() + 1e-5, (k, err)
+        dy = torch.from_numpy(rng_array(tuple(r.shape), 100 + k))
+        loss_g = loss_g + (nhwc_to_nchw(a) * dy.float().to(DEV)).sum()
+        loss_r = loss_r + (r * dy).sum()
+    loss_g.backward()
+    loss_r.backward()
+    for k, p in net.named_parameters():
+        ref = P[k].grad
+        err = (p.grad.double().cpu() - ref).abs().max().item()
+        assert err <= 2e-3 * ref.abs().max().item() + 1e-6, (k, err, ref.abs().max().item())
+
+
+def test_adabins_end_to_end_vs_oracle():
+    """Whole UnetAdaptiveBins (restated B5 encoder + reference-pinned head) vs the CPU oracle."""
+    from mdemi.model.Adabins import UnetAdaptiveBins
+    from oracle import adabins as oab
+    from oracle.weights import rng_array
+    m = UnetAdaptiveBins.build(256, 1e-3, 10.0)
+    P = _oracle_params(m, 0.41, 0.03)
+    m = m.to(DEV).train()
+    img = torch.from_numpy(rng_array((2, 3, 352, 384), 78))
+    pred, edges = m(img.float().to(DEV))
+    pr, er = oab.unet_adaptive_bins(P, img.double(), 1e-3, 10.0)
+    for a, r in ((pred, pr), (edges, er)):
+        err = (a.double().cpu() - r).abs().max().item()
+        assert err <= 1e-4 * r.abs().max().item(), err
+    dy = torch.from_numpy(rng_array(tuple(pr.shape), 79))
+    (pred * dy.float().to(DEV)).sum().backward()
+    (pr * dy).sum().backward()
+    worst = 0.0
+    for k, p in m.named_parameters():
+        ref = P[k].grad
+        rel = (p.grad.double().cpu() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
+        worst = max(worst, rel if ref.abs().max().item() > 1e-9 else 0.0)
+    assert worst <= 5e-3, worst

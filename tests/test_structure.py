@@ -1,7 +1,7 @@
 """CPU checks of the drop-in boundary: the mdemi model mirrors expose the
 reference's state_dict (same keys, shapes, dtypes and order — the order also
 drives the closed-form weight fill) and the C-ABI library exports every
-symbol include/mdemi.h declares."""
+symbol include/mdemi.h and include/mdemi_ext.h declare."""
 import os
 import re
 
@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_every_header_symbol():
     from mdemi import _lib
     lib = _lib.load()
-    header = open(_lib.HEADER_PATH).read()
+    header = "".join(open(h).read() for h in _lib.HEADER_PATHS)
     declared = set(re.findall(r"\b(mdemi_[a-z0-9_]+)\s*\(", header))
     assert len(declared) > 30
     for name in sorted(declared):
@@ -72,3 +72,30 @@ def test_large07_parameter_count():
     m = NewCRFDepth(version="large07", max_depth=10.0)
     assert sum(p.numel() for p in m.parameters()) == 270_444_877
     assert sum(p.numel() for p in m.backbone.parameters()) == 194_998_164
+
+
+def _fake_backend():
+    import torch.nn as nn
+    m = nn.Module()
+    m.conv_stem, m.bn1, m.act1 = nn.Identity(), nn.Identity(), nn.Identity()
+    m.blocks = nn.Sequential(*[nn.Identity() for _ in range(7)])
+    m.conv_head, m.act2 = nn.Identity(), nn.Identity()
+    return m
+
+
+def test_state_dict_matches_reference_adabins():
+    from mdemi.model.Adabins import UnetAdaptiveBins, mViT
+    _spec_eq(UnetAdaptiveBins(_fake_backend(), n_bins=256, min_val=1e-3, max_val=10.0), "adabins_head")
+    _spec_eq(mViT(128, n_query_channels=128, patch_size=16, dim_out=256, embedding_dim=128, norm="linear"), "mvit")
+
+
+def test_adabins_parameter_counts():
+    """AdaBins non-encoder params 49,916,544; EfficientNet-B5 28.34 M incl. conv_head."""
+    from mdemi.model.Adabins import UnetAdaptiveBins
+    m = UnetAdaptiveBins.build(256, 1e-3, 10.0)
+    enc = sum(p.numel() for p in m.encoder.parameters())
+    assert sum(p.numel() for p in m.parameters()) - enc == 49_916_544
+    assert enc == 28_336_688
+    keys = list(m.state_dict().keys())
+    assert keys[0] == "encoder.original_model.conv_stem.weight"
+    assert "encoder.original_model.blocks.6.2.se.conv_expand.bias" in keys
