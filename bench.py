@@ -89,63 +89,6 @@ def build(args, device):
     return model, opt, loss_fn
 
 
-class GradAllReduce:
-    """Bucketed fp32 gradient all-reduce over RCCL (torch.distributed 'nccl' == RCCL on ROCm),
-    launched from post-accumulate hooks in reverse registration order so buckets
-    overlap the rest of the backward; mean = sum / world (DDP semantics)."""
-
-    def __init__(self, model, bucket_mb=64):
-        self.world = dist.get_world_size()
-        self.params = [p for p in model.parameters() if p.requires_grad]
-        self.buckets, cur, size = [], [], 0
-        for p in reversed(self.params):
-            cur.append(p)
-            size += p.numel() * 4
-            if size >= bucket_mb * 2 ** 20:
-                self.buckets.append(cur)
-                cur, size = [], 0
-        if cur:
-            self.buckets.append(cur)
-        self.bucket_of = {}
-        for bi, b in enumerate(self.buckets):
-            for p in b:
-                self.bucket_of[p] = bi
-        self.pending = [0] * len(self.buckets)
-        self.works = []
-        self.flat = [None] * len(self.buckets)
-        for p in self.params:
-            p.register_post_accumulate_grad_hook(self._hook)
-        self.reset()
-
-    def reset(self):
-        self.pending = [len(b) for b in self.buckets]
-        self.works = []
-
-    def _hook(self, p):
-        bi = self.bucket_of[p]
-        self.pending[bi] -= 1
-        if self.pending[bi] == 0:
-            from mdemi import functional as mf
-            grads = [q.grad for q in self.buckets[bi]]
-            flat = mf.concat_channels([g.reshape(1, -1) for g in grads]).view(-1)
-            self.flat[bi] = (flat, grads)
-            self.works.append(dist.all_reduce(flat, async_op=True))
-
-    def finish(self):
-        from mdemi import _lib as L
-        for w in self.works:
-            w.wait()
-        for flat, grads in filter(None, self.flat):
-            off = 0
-            for g in grads:
-                n = g.numel()
-                L.call("mdemi_elementwise", L.EW_AXPBY, flat[off:off + n].data_ptr(), flat[off:off + n].data_ptr(),
-                       g.data_ptr(), n, 1.0 / self.world, 0.0, L.stream())
-                off += n
-        self.flat = [None] * len(self.buckets)
-        self.reset()
-
-
 def train_step(model, opt, loss_fn, img, gt, ddp=None):
     pred = model(img)
     loss = loss_fn(pred, gt)
@@ -256,10 +199,11 @@ def main():
     W = args.width or cfg["w"]
 
     model, opt, loss_fn = build(args, device)
-    ddp = GradAllReduce(model) if world > 1 else None
-    if world > 1:  # identical replicas (DDP broadcasts rank 0's weights)
-        for p in model.state_dict().values():
-            dist.broadcast(p, 0)
+    ddp = None
+    if world > 1:  # bucketed RCCL gradient mean overlapped with backward (mdemi/train/ddp.py)
+        from mdemi.train import GradAllReduce, broadcast_parameters
+        broadcast_parameters(model)  # identical replicas (DDP broadcasts rank 0's weights)
+        ddp = GradAllReduce(model, bucket_mb=64.0)
     img, gt = synthetic_batch(B, H, W, device, seed=1000 + rank)
 
     for _ in range(args.warmup):

@@ -72,6 +72,11 @@ int mdemi_softmax_fwd(const float* x, float* y, int64_t rows, int32_t cols, floa
 int mdemi_softmax_bwd(const float* y, const float* dy, float* dx, int64_t rows, int32_t cols, float scale,
                       int32_t accumulate, void* stream);
 
+/* y = act(x) elementwise (MDEMI_ACT_* code): the standalone activations of
+ * UpscaleConcatAct (layer_utils.py:121) and the bin regressor
+ * (decoder_v8.py:82-90).  The backward is mdemi_elementwise(MDEMI_EW_ACT_BWD). */
+int mdemi_act_fwd(const float* x, float* y, int64_t n, int32_t act, void* stream);
+
 /* Inverted dropout with a counter-based mask: y = x * keep(seed, offset+i) / (1-p).
  * The mask is a pure function of (seed, offset, i), so the backward is the
  * same call on dy (nn.Dropout in layers.py:8, luna_layer.py:172-173,
@@ -112,6 +117,12 @@ int mdemi_bins_bwd(const float* raw, const float* dcenters, const float* dedges,
 /* NCHW -> NHWC with the channel dim zero-padded to Cp >= C (the 3-channel    */
 /* image feeding EfficientNet's conv_stem through the implicit-GEMM conv).   */
 int mdemi_nchw_to_nhwc_pad(const float* x, float* y, int32_t N, int32_t C, int64_t HW, int32_t Cp, void* stream);
+/* Input gradient of a stride == kernel conv (no padding) over NHWC, the
+ * scatter of its im2col columns (mViT's 16x16/16 embedding_encoder,
+ * layers.py:13-18): x[n][y][x][c] = cols[(n*OH + y/p)*OW + x/p][((y%p)*p + x%p)*C + c]
+ * for y < OH*p, x < OW*p; other pixels (dropped by the floor) get 0. */
+int mdemi_unpatchify_nhwc(const float* cols, float* x, int32_t N, int32_t H, int32_t W, int32_t C, int32_t p,
+                          int32_t OH, int32_t OW, void* stream);
 /* Adjoint of replicate padding by p (padding_mode="replicate",              */
 /* layer_utils.py:18-22): dx[n][y][x] = sum of dxp over the padded positions */
 /* that clamp to (y, x).  dxp is [N][H+2p][W+2p][C].                          */

@@ -107,13 +107,15 @@ __global__ void bn_bwd_combine(const float* __restrict__ part, int nblk, int C, 
                                float* __restrict__ dbeta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float a = 0.f, b = 0.f;
+  // fp64 combine, as for the forward statistics: dx subtracts these means
+  // from d, so their rounding is what survives the cancellation
+  double a = 0.0, b = 0.0;
   for (int i = 0; i < nblk; ++i) {
-    a += part[((int64_t)i * 2 + 0) * C + c];
-    b += part[((int64_t)i * 2 + 1) * C + c];
+    a += (double)part[((int64_t)i * 2 + 0) * C + c];
+    b += (double)part[((int64_t)i * 2 + 1) * C + c];
   }
-  dgamma[c] = a;
-  dbeta[c] = b;
+  dgamma[c] = (float)a;
+  dbeta[c] = (float)b;
 }
 
 __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply(const float* __restrict__ dy, const float* __restrict__ x,

@@ -250,9 +250,9 @@ __global__ __launch_bounds__(256) void spatial_final(const float* __restrict__ p
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)N * C) return;
   const int n = (int)(e / C), c = (int)(e % C);
-  float s = 0.f;
-  for (int k = 0; k < nchunk; ++k) s += part[((int64_t)n * nchunk + k) * C + c];
-  out[e] = s * scale;
+  double s = 0.0;  // fixed-order fp64 combine of the chunk partials
+  for (int k = 0; k < nchunk; ++k) s += (double)part[((int64_t)n * nchunk + k) * C + c];
+  out[e] = (float)(s * (double)scale);
 }
 
 static int spatial_chunks(int N, int64_t HW, int C) {
@@ -359,24 +359,24 @@ __global__ __launch_bounds__(256) void se_gate_wgrad_kernel(const float* __restr
   const int64_t RC = (int64_t)R * C;
   const int64_t total = 2 * RC + C + R;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    float s = 0.f;
+    double s = 0.0;  // sums over the N images in fp64 (N is small; these are tiny tensors)
     if (e < RC) {  // dwr[r][c] = sum_n dz[n][r] * pooled[n][c]
       const int r = (int)(e / C), c = (int)(e % C);
-      for (int n = 0; n < N; ++n) s = fmaf(dz[(int64_t)n * R + r], pooled[(int64_t)n * C + c], s);
-      dwr[e] = s;
+      for (int n = 0; n < N; ++n) s += (double)dz[(int64_t)n * R + r] * pooled[(int64_t)n * C + c];
+      dwr[e] = (float)s;
     } else if (e < 2 * RC) {  // dwe[c][r] = sum_n de[n][c] * silu(hid[n][r])
       const int64_t f = e - RC;
       const int c = (int)(f / R), r = (int)(f % R);
-      for (int n = 0; n < N; ++n) s = fmaf(de[(int64_t)n * C + c], silu_f(hid[(int64_t)n * R + r]), s);
-      dwe[f] = s;
+      for (int n = 0; n < N; ++n) s += (double)de[(int64_t)n * C + c] * silu_f(hid[(int64_t)n * R + r]);
+      dwe[f] = (float)s;
     } else if (e < 2 * RC + C) {
       const int c = (int)(e - 2 * RC);
       for (int n = 0; n < N; ++n) s += de[(int64_t)n * C + c];
-      dbe[c] = s;
+      dbe[c] = (float)s;
     } else {
       const int r = (int)(e - 2 * RC - C);
       for (int n = 0; n < N; ++n) s += dz[(int64_t)n * R + r];
-      dbr[r] = s;
+      dbr[r] = (float)s;
     }
   }
 }

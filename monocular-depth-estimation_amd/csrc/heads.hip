@@ -154,6 +154,12 @@ __global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ 
     y[i] = uniform01(seed, offset + (uint64_t)i) >= p ? x[i] * inv_keep : 0.f;
 }
 
+__global__ __launch_bounds__(256) void act_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                                                      int act) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    y[i] = apply_act(act, x[i]);
+}
+
 // ---------------------------------------------------------------------------
 // channels-last bin head: one wave per pixel row of K bins (K % 4 == 0)
 // ---------------------------------------------------------------------------
@@ -330,6 +336,26 @@ __global__ __launch_bounds__(256) void pad_fold_kernel(const float* __restrict__
   }
 }
 
+__global__ __launch_bounds__(256) void unpatchify_kernel(const float* __restrict__ cols, float* __restrict__ x, int N,
+                                                         int H, int W, int C, int p, int OH, int OW) {
+  const int C4 = C >> 2;
+  const int64_t total = (int64_t)N * H * W * C4;
+  const int64_t K = (int64_t)p * p * C;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c4 = (int)(e % C4);
+    int64_t t = e / C4;
+    const int xx = (int)(t % W); t /= W;
+    const int yy = (int)(t % H);
+    const int n = (int)(t / H);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (yy < OH * p && xx < OW * p) {
+      const int64_t row = ((int64_t)n * OH + yy / p) * OW + xx / p;
+      v = *reinterpret_cast<const float4*>(cols + row * K + ((int64_t)(yy % p) * p + xx % p) * C + c4 * 4);
+    }
+    reinterpret_cast<float4*>(x)[e] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // depth metrics: grid (chunks, B); 11 sums per image
 // ---------------------------------------------------------------------------
@@ -451,6 +477,12 @@ extern "C" int mdemi_dropout(const float* x, float* y, int64_t n, float p, uint6
   return check_launch("dropout");
 }
 
+extern "C" int mdemi_act_fwd(const float* x, float* y, int64_t n, int32_t act, void* stream) {
+  MDEMI_REQUIRE(x && y && n > 0, "act_fwd: bad args");
+  hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, act);
+  return check_launch("act_fwd");
+}
+
 extern "C" int mdemi_binhead_nhwc_fwd(const float* logits, const float* centers, float* pred, float* stats, int32_t B,
                                       int64_t HW, int32_t K, void* stream) {
   MDEMI_REQUIRE(logits && centers && pred && stats && B > 0 && HW > 0 && K > 0 && K % 4 == 0,
@@ -498,6 +530,16 @@ extern "C" int mdemi_bins_bwd(const float* raw, const float* dcenters, const flo
   hipLaunchKernelGGL(bins_bwd_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, (hipStream_t)stream, raw, dcenters,
                      dedges, dwidths_n, draw, B, K, mode, min_val, max_val);
   return check_launch("bins_bwd");
+}
+
+extern "C" int mdemi_unpatchify_nhwc(const float* cols, float* x, int32_t N, int32_t H, int32_t W, int32_t C,
+                                     int32_t p, int32_t OH, int32_t OW, void* stream) {
+  MDEMI_REQUIRE(cols && x && N > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0 && p > 0 && OH * p <= H && OW * p <= W,
+                "unpatchify_nhwc: bad args (C %% 4 == 0)");
+  const int64_t total = (int64_t)N * H * W * (C / 4);
+  hipLaunchKernelGGL(unpatchify_kernel, dim3(grid_1d(total)), dim3(256), 0, (hipStream_t)stream, cols, x, N, H, W, C, p,
+                     OH, OW);
+  return check_launch("unpatchify_nhwc");
 }
 
 extern "C" int mdemi_pad_fold_replicate(const float* dxp, float* dx, int32_t N, int32_t H, int32_t W, int32_t C,

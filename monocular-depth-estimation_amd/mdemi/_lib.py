@@ -153,6 +153,7 @@ _SIGS = {
     "mdemi_se_gate_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "mdemi_softmax_fwd": (ctypes.c_int, [vp, vp, i64, i32, f32, vp]),
     "mdemi_softmax_bwd": (ctypes.c_int, [vp, vp, vp, i64, i32, f32, i32, vp]),
+    "mdemi_act_fwd": (ctypes.c_int, [vp, vp, i64, i32, vp]),
     "mdemi_dropout": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "mdemi_binhead_nhwc_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, vp]),
     "mdemi_binhead_nhwc_bwd_workspace_size": (sz, [i32, i64, i32]),
@@ -160,6 +161,7 @@ _SIGS = {
     "mdemi_bins_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, f32, f32, vp]),
     "mdemi_bins_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, vp]),
     "mdemi_nchw_to_nhwc_pad": (ctypes.c_int, [vp, vp, i32, i32, i64, i32, vp]),
+    "mdemi_unpatchify_nhwc": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mdemi_pad_fold_replicate": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
     "mdemi_depth_metrics_workspace_size": (sz, [i32, i32, i32]),
     "mdemi_depth_metrics": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, f32, i32, vp, vp, vp]),

@@ -309,9 +309,18 @@ class _Conv2dFn(torch.autograd.Function):
                 dx = torch.empty_like(x)
                 gemm(dy, weight.reshape(cout, cin), dx, M, c, cout, lda=cout, ldb=cin, ldc=c,
                      a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
+            elif stride == kh == kw and pad == 0 and not ctx.explicit:
+                # non-overlapping patches (mViT embedding_encoder): column gradients by one GEMM
+                # against the (ky,kx,c)-ordered weight, then a scatter back to the NHWC pixels
+                wf = weight.permute(0, 2, 3, 1).reshape(cout, K).contiguous()
+                dcols = torch.empty(M, K, device=dy.device, dtype=torch.float32)
+                gemm(dy, wf, dcols, M, K, cout, lda=cout, ldb=K, ldc=K, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
+                dx = torch.empty_like(x)
+                L.call("mdemi_unpatchify_nhwc", dcols.data_ptr(), dx.data_ptr(), n, h, w, c, stride, oh, ow,
+                       L.stream())
             else:
                 if stride != 1 or ctx.explicit:
-                    raise NotImplementedError("conv2d dgrad: stride 1 only")
+                    raise NotImplementedError("conv2d dgrad: stride 1 or stride == kernel only")
                 # dX = conv(dY, flip(W)^T) with pad k-1-p:  Wd[(ky,kx,co)][c] = W[co][c][k-1-ky][k-1-kx]
                 wd = weight.flip(2, 3).permute(2, 3, 0, 1).reshape(kh * kw * cout, cin).contiguous()
                 dx = torch.empty_like(x)
@@ -1615,3 +1624,78 @@ class _AddRowsBroadcastFn(torch.autograd.Function):
 
 def add_rows_broadcast(x, table):
     return _AddRowsBroadcastFn.apply(x, table)
+
+
+class _ActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        _require_cuda(x)
+        x = _c(x)
+        y = torch.empty_like(x)
+        L.call("mdemi_act_fwd", x.data_ptr(), y.data_ptr(), x.numel(), act, L.stream())
+        ctx.save_for_backward(x)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = _c(dy)
+        dx = torch.empty_like(x)
+        L.call("mdemi_elementwise", L.EW_ACT_BWD, x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(),
+               float(ctx.act), 0.0, L.stream())
+        return dx, None
+
+
+def activation(x, act):
+    """act(x) elementwise (L.ACT_*)."""
+    if act == L.ACT_NONE:
+        return x
+    return _ActFn.apply(x, act)
+
+
+class _ResizeConcatFn(torch.autograd.Function):
+    """cat([resize(p) for p in pieces], channels) with each bilinear resize (or plain copy when
+    the size already matches) written straight into its channel slice (decoder_v8.py:152-156)."""
+
+    @staticmethod
+    def forward(ctx, size, align, *pieces):
+        _require_cuda(*pieces)
+        pieces = [_c(p) for p in pieces]
+        n = pieces[0].shape[0]
+        oh, ow = size
+        widths = [p.shape[-1] for p in pieces]
+        ct = sum(widths)
+        out = torch.empty(n, oh, ow, ct, device=pieces[0].device, dtype=torch.float32)
+        off = 0
+        for p, wd in zip(pieces, widths):
+            _, h, w, _ = p.shape
+            if (h, w) == (oh, ow):
+                _copy2d(p.view(-1, wd), out.view(-1, ct)[:, off:off + wd])
+            else:
+                L.call("mdemi_bilinear_fwd", p.data_ptr(), out.data_ptr() + 4 * off, n, h, w, wd, oh, ow, int(align),
+                       0.0, 0.0, wd, ct, L.stream())
+            off += wd
+        ctx.shapes = [tuple(p.shape) for p in pieces]
+        ctx.cfg = (oh, ow, align, ct)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        oh, ow, align, ct = ctx.cfg
+        dy = _c(dy)
+        grads, off = [], 0
+        for (n, h, w, wd) in ctx.shapes:
+            g = torch.empty(n, h, w, wd, device=dy.device, dtype=torch.float32)
+            if (h, w) == (oh, ow):
+                _copy2d(dy.view(-1, ct)[:, off:off + wd], g.view(-1, wd))
+            else:
+                L.call("mdemi_bilinear_bwd", dy.data_ptr() + 4 * off, g.data_ptr(), n, h, w, wd, oh, ow, int(align),
+                       0.0, 0.0, ct, wd, 0, L.stream())
+            grads.append(g)
+            off += wd
+        return (None, None) + tuple(grads)
+
+
+def resize_concat(pieces, size, align_corners=True):
+    return _ResizeConcatFn.apply(tuple(size), align_corners, *pieces)

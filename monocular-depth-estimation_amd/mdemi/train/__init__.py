@@ -5,3 +5,4 @@ loss.*, optimizer.*, scheduler.*, train.*).  Parity for these is unpinned;
 choices are documented in DESIGN.md."""
 from .optim import FusedAdamW, OneCycleLR  # noqa: F401
 from .loss import SILogLoss  # noqa: F401
+from .ddp import GradAllReduce, broadcast_parameters  # noqa: F401

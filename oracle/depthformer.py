@@ -145,3 +145,11 @@ def depthformer_v8(P, feats, opt, min_depth, max_depth):  # depthformer_v8.py:46
     centers = (0.5 * (edges[..., :-1] + edges[..., 1:])).unsqueeze(-1).unsqueeze(-1)
     depth = torch.sum(bin_cls * centers, dim=1, keepdim=True)
     return depth, centers, attn
+
+
+def depthformer_v8_full(P, x, opt, min_depth, max_depth):
+    """Whole DepthformerV8.forward (depthformer_v8.py:46-75) with the restated EfficientNet-B5
+    encoder (oracle/efficientnet.py — parity unpinned)."""
+    from . import efficientnet as oeff
+    f = oeff.features(P, "encoder.backend.", x, last=10)
+    return depthformer_v8(P, (f[4], f[5], f[6], f[8], f[10]), opt, min_depth, max_depth)

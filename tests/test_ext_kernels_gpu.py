@@ -306,3 +306,21 @@ def test_depth_metrics_match_reference_golden(mf):
         for i, nme in enumerate(names):
             ref = float(d[f"err/{case}/{nme}"])
             assert abs(out[i] - ref) <= 2e-6 * abs(ref) + 1e-9, (case, nme, out[i], ref)
+
+
+def test_patch_conv_dgrad(mf):
+    """stride == kernel conv (mViT embedding_encoder, layers.py:13-18): input gradient by column
+    GEMM + NHWC scatter; rows/cols dropped by the floor get zero."""
+    x, w, b = rnd(2, 8, 13, 17, seed=50), rnd(12, 8, 4, 4, seed=51, scale=0.3), rnd(12, seed=52)
+    xr, wr, br = [t.clone().requires_grad_() for t in (x, w, b)]
+    yr = F.conv2d(xr, wr, br, stride=4)
+    dy = rnd(*yr.shape, seed=53)
+    yr.backward(dy)
+    xg, wg, bg = nhwc(x).float().to(DEV).requires_grad_(), w.float().to(DEV).requires_grad_(), \
+        b.float().to(DEV).requires_grad_()
+    yg = mf.conv2d_nhwc(xg, wg, bg, stride=4, pad=0)
+    yg.backward(nhwc(dy).float().to(DEV))
+    close(nchw(yg), yr, rtol=1e-4)
+    close(nchw(xg.grad), xr.grad, rtol=1e-4)
+    close(wg.grad, wr.grad, rtol=1e-4)
+    close(bg.grad, br.grad, rtol=1e-4)

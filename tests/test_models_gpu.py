@@ -26,6 +26,11 @@ def load_golden_weights(model, g):
     sd = model.state_dict()
     cpu = {k: v.detach().cpu().clone() for k, v in sd.items()}
     closed_form_fill(cpu, seed=g.fill[0], scale=g.fill[1])
+    for mod in model.modules():  # the fixtures were generated with dropout off (make_golden.prep)
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+        if isinstance(mod, torch.nn.MultiheadAttention):
+            mod.dropout = 0.0
     with torch.no_grad():
         for k, v in sd.items():
             if torch.is_floating_point(v):
@@ -158,7 +163,7 @@ class _Const(torch.nn.Module):
         self.idx = idx
 
     def forward(self, x):
-        return self._holder[self.idx]
+        return self._holder.get(self.idx, x)
 
 
 def fake_backend(holder):
@@ -168,6 +173,42 @@ def fake_backend(holder):
     m.blocks = torch.nn.Sequential(*[_Const(holder, 4 + i) for i in range(7)])
     m.conv_head, m.act2 = _Const(holder, 11), _Const(holder, 12)
     return m
+
+
+def oracle_grads(g, oracle_fn, out_names, dtype):
+    """Oracle forward+backward of L = sum(out * dy) on the golden weights/inputs in `dtype`."""
+    P = g.params(dtype)
+    for v in P.values():
+        if torch.is_floating_point(v):
+            v.requires_grad_(True)
+    ins = {n: g.input(n, dtype).requires_grad_(True) for n in g.input_names()}
+    outs = oracle_fn(P, ins)
+    loss = 0
+    for name, o in zip(out_names, outs):
+        loss = loss + (o * g.dy(name, o.shape, dtype)).sum()
+    loss.backward()
+    return P, ins
+
+
+def check_grads_conditioned(g, model, ins, in_layouts, oracle_fn, out_names, slack=20.0):
+    """Gradients of deep BatchNorm decoders at batch 1 are ill-conditioned: the reference's own fp32
+    gradients differ from fp64 by up to ~3e-2 relative (the pre-BN conv biases, exactly zero in exact
+    arithmetic, are pure rounding noise).  So the GPU gradients are held to the fp64 oracle (pinned to
+    the reference by tests/test_oracle_golden.py) within `slack` x the fp32 CPU error of the same
+    computation, plus 1e-4 relative."""
+    P64, I64 = oracle_grads(g, oracle_fn, out_names, torch.float64)
+    P32, I32 = oracle_grads(g, oracle_fn, out_names, torch.float32)
+    checked = 0
+    pairs = [(k, p.grad, P64[k].grad, P32[k].grad) for k, p in model.named_parameters()]
+    pairs += [(n, nhwc_to_nchw(t.grad) if in_layouts.get(n) == "nchw" else t.grad, I64[n].grad, I32[n].grad)
+              for n, t in ins.items()]
+    for k, got, r64, r32 in pairs:
+        e_gpu = (got.double().cpu() - r64).abs().max().item()
+        e_cpu = (r32.double() - r64).abs().max().item()
+        mag = r64.abs().max().item()
+        assert e_gpu <= slack * e_cpu + 1e-4 * mag + 1e-9, (k, e_gpu, e_cpu, mag)
+        checked += 1
+    return checked
 
 
 def test_adabins_head():
@@ -183,8 +224,18 @@ def test_adabins_head():
             holder[int(k[1:])] = v
         return m(torch.zeros(1, 3, 8, 8, device=DEV))
 
-    n = run_case(g, m, fwd, ["pred", "bin_edges"], {}, {k: "nchw" for k in g.input_names()})
-    assert n == len(list(m.parameters()))
+    lay = {k: "nchw" for k in g.input_names()}
+    model = load_golden_weights(m.to(DEV), g).train()
+    ins = {n: nchw_to_nhwc(g.input(n, torch.float32)).to(DEV).requires_grad_(True) for n in g.input_names()}
+    pred, edges = fwd(model, ins)
+    g.check("out/pred", pred.float().cpu(), RT_OUT, 1e-5)
+    g.check("out/bin_edges", edges.float().cpu(), RT_OUT, 1e-5)
+    ((pred * g.dy("pred", pred.shape, torch.float32).to(DEV)).sum() +
+     (edges * g.dy("bin_edges", edges.shape, torch.float32).to(DEV)).sum()).backward()
+    from oracle import adabins as oab
+    n = check_grads_conditioned(g, model, ins, lay, lambda P, i: oab.adabins_head(
+        P, {int(k[1:]): v for k, v in i.items()}, 1e-3, 10.0), ["pred", "bin_edges"])
+    assert n == len(list(m.parameters())) + len(ins)
 
 
 def test_mvit():
@@ -196,41 +247,72 @@ def test_mvit():
     assert n == len(list(m.parameters()))
 
 
-def _oracle_params(model, seed, scale):
+def _filled_state(model, seed, scale):
+    """Closed-form weights (oracle/weights.py) loaded into `model`; returns the CPU state dict."""
     from oracle.weights import closed_form_fill
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     closed_form_fill(sd, seed=seed, scale=scale)
     model.load_state_dict(sd)
-    return {k: (v.double().requires_grad_(True) if torch.is_floating_point(v) else v) for k, v in sd.items()}
+    return sd
+
+
+def _oracle_run(sd, dtype, loss_fn):
+    P = {k: (v.to(dtype).requires_grad_(True) if torch.is_floating_point(v) else v) for k, v in sd.items()}
+    outs = loss_fn(P)
+    return P, outs
+
+
+def _check_param_grads(model, sd, loss_fn, slack=20.0):
+    """GPU parameter gradients vs the fp64 oracle, within `slack` x the fp32 oracle's own error
+    (BatchNorm stacks make some gradients -- e.g. biases feeding a BN, exactly zero in exact
+    arithmetic -- pure rounding noise) plus 1e-4 relative."""
+    P64, _ = _oracle_run(sd, torch.float64, loss_fn)
+    P32, _ = _oracle_run(sd, torch.float32, loss_fn)
+    n = 0
+    for k, p in model.named_parameters():
+        r64, r32 = P64[k].grad, P32[k].grad
+        if r64 is None:
+            assert p.grad is None or p.grad.abs().max().item() == 0, k
+            continue
+        e_gpu = (p.grad.double().cpu() - r64).abs().max().item()
+        e_cpu = (r32.double() - r64).abs().max().item()
+        mag = r64.abs().max().item()
+        assert e_gpu <= slack * e_cpu + 1e-4 * mag + 1e-9, (k, e_gpu, e_cpu, mag)
+        n += 1
+    return n
 
 
 def test_efficientnet_b5_encoder_vs_oracle():
-    """Restated tf_efficientnet_b5_ap (parity unpinned: third-party, not offline) — libmdemi vs the
+    """Restated tf_efficientnet_b5_ap (parity unpinned: third-party, not offline) -- libmdemi vs the
     CPU oracle restatement on the same closed-form weights: features [4,5,6,8,11] and all grads."""
     from mdemi.model.gen_efficientnet import tf_efficientnet_b5_ap, walk_features
     from oracle import efficientnet as oeff
     from oracle.weights import rng_array
     net = tf_efficientnet_b5_ap()
     del net.bn2, net.global_pool, net.classifier
-    P = _oracle_params(net, 0.31, 0.05)
+    sd = _filled_state(net, 0.31, 0.05)
     net = net.to(DEV).train()
     img = torch.from_numpy(rng_array((2, 3, 64, 96), 77))
     fg = walk_features(net, img.float().to(DEV), 11)
-    fr = oeff.features(P, "", img.double(), 11)
-    loss_g, loss_r = 0, 0
+    dys = {}
+    loss_g = 0
+    with torch.no_grad():
+        fr = oeff.features({k: v.double() if torch.is_floating_point(v) else v for k, v in sd.items()}, "",
+                           img.double(), 11)
     for k in (4, 5, 6, 8, 11):
         a, r = fg[k], fr[k]
         err = (nhwc_to_nchw(a).double().cpu() - r).abs().max().item()
         assert err <= 1e-4 * r.abs().max().item() + 1e-5, (k, err)
-        dy = torch.from_numpy(rng_array(tuple(r.shape), 100 + k))
-        loss_g = loss_g + (nhwc_to_nchw(a) * dy.float().to(DEV)).sum()
-        loss_r = loss_r + (r * dy).sum()
+        dys[k] = torch.from_numpy(rng_array(tuple(r.shape), 100 + k))
+        loss_g = loss_g + (nhwc_to_nchw(a) * dys[k].float().to(DEV)).sum()
     loss_g.backward()
-    loss_r.backward()
-    for k, p in net.named_parameters():
-        ref = P[k].grad
-        err = (p.grad.double().cpu() - ref).abs().max().item()
-        assert err <= 2e-3 * ref.abs().max().item() + 1e-6, (k, err, ref.abs().max().item())
+
+    def loss_fn(P):
+        f = oeff.features(P, "", img.to(P["conv_stem.weight"].dtype), 11)
+        loss = sum((f[k] * dys[k].to(f[k].dtype)).sum() for k in dys)
+        loss.backward()
+
+    assert _check_param_grads(net, sd, loss_fn) == len(list(net.parameters()))
 
 
 def test_adabins_end_to_end_vs_oracle():
@@ -239,20 +321,76 @@ def test_adabins_end_to_end_vs_oracle():
     from oracle import adabins as oab
     from oracle.weights import rng_array
     m = UnetAdaptiveBins.build(256, 1e-3, 10.0)
-    P = _oracle_params(m, 0.41, 0.03)
+    sd = _filled_state(m, 0.41, 0.03)
     m = m.to(DEV).train()
     img = torch.from_numpy(rng_array((2, 3, 352, 384), 78))
     pred, edges = m(img.float().to(DEV))
-    pr, er = oab.unet_adaptive_bins(P, img.double(), 1e-3, 10.0)
+    with torch.no_grad():
+        pr, er = oab.unet_adaptive_bins({k: v.double() if torch.is_floating_point(v) else v for k, v in sd.items()},
+                                        img.double(), 1e-3, 10.0)
     for a, r in ((pred, pr), (edges, er)):
         err = (a.double().cpu() - r).abs().max().item()
         assert err <= 1e-4 * r.abs().max().item(), err
     dy = torch.from_numpy(rng_array(tuple(pr.shape), 79))
     (pred * dy.float().to(DEV)).sum().backward()
-    (pr * dy).sum().backward()
-    worst = 0.0
-    for k, p in m.named_parameters():
-        ref = P[k].grad
-        rel = (p.grad.double().cpu() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
-        worst = max(worst, rel if ref.abs().max().item() > 1e-9 else 0.0)
-    assert worst <= 5e-3, worst
+
+    def loss_fn(P):
+        p, _ = oab.unet_adaptive_bins(P, img.to(P["conv_out.0.weight"].dtype), 1e-3, 10.0)
+        (p * dy.to(p.dtype)).sum().backward()
+
+    assert _check_param_grads(m, sd, loss_fn) == len(list(m.parameters()))
+
+
+# ---------------------------------------------------------------------------
+# Depthformer v8 (model/Depthformer)
+# ---------------------------------------------------------------------------
+DFV8_OPT = {"hidden_dim": 64, "num_heads": 4, "num_bins": 32, "num_aux": 16, "img_size": [64, 96],
+            "attn_drop_prob": 0.0, "drop_prob": 0.0}
+
+
+def test_depthformer_v8_decoder_and_head():
+    """Decoder (Luna x4, ViT aux layer, ResConvBN with replicate padding, shoot heads) + bin head
+    vs the reference, EfficientNet features as stored maps; depth, centres and all 8 attention maps."""
+    from mdemi.model.Depthformer import DepthformerV8
+    g = Golden("depthformer_v8")
+    holder = {}
+    m = DepthformerV8(fake_backend(holder), DFV8_OPT, min_depth=1e-3, max_depth=10.0)
+
+    def fwd(m, i):
+        holder.clear()
+        for k, v in i.items():
+            holder[int(k[1:])] = v
+        depth, centers, attn = m(torch.zeros(2, 3, 8, 8, device=DEV))
+        return (depth, centers) + tuple(attn)
+
+    n = run_case(g, m, fwd, ["depth", "centers"] + [f"attn{k}" for k in range(8)], {},
+                 {k: "nchw" for k in g.input_names()})
+    assert n == len(list(m.parameters()))
+
+
+def test_depthformer_v8_end_to_end_vs_oracle():
+    """Whole DepthformerV8 (restated B5 encoder + reference-pinned decoder) vs the CPU oracle."""
+    from mdemi.model.Depthformer import DepthformerV8
+    from oracle import depthformer as odf
+    from oracle.weights import rng_array
+    opt = {"hidden_dim": 64, "num_heads": 4, "num_bins": 64, "num_aux": 32, "img_size": [128, 160],
+           "attn_drop_prob": 0.0, "drop_prob": 0.0}
+    m = DepthformerV8.build(opt, 1e-3, 10.0)
+    sd = _filled_state(m, 0.51, 0.03)
+    m = m.to(DEV).train()
+    img = torch.from_numpy(rng_array((2, 3, 128, 160), 80))
+    depth, centers, attn = m(img.float().to(DEV))
+    with torch.no_grad():
+        dr, cr, ar = odf.depthformer_v8_full({k: v.double() if torch.is_floating_point(v) else v
+                                              for k, v in sd.items()}, img.double(), opt, 1e-3, 10.0)
+    for a, r in [(depth, dr), (centers, cr)] + list(zip(attn, ar)):
+        err = (a.double().cpu() - r).abs().max().item()
+        assert err <= 1e-4 * r.abs().max().item(), err
+    dy = torch.from_numpy(rng_array(tuple(dr.shape), 81))
+    (depth * dy.float().to(DEV)).sum().backward()
+
+    def loss_fn(P):
+        d, _, _ = odf.depthformer_v8_full(P, img.to(P["decoder.aux_embedding"].dtype), opt, 1e-3, 10.0)
+        (d * dy.to(d.dtype)).sum().backward()
+
+    assert _check_param_grads(m, sd, loss_fn) > 0

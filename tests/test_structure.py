@@ -99,3 +99,21 @@ def test_adabins_parameter_counts():
     keys = list(m.state_dict().keys())
     assert keys[0] == "encoder.original_model.conv_stem.weight"
     assert "encoder.original_model.blocks.6.2.se.conv_expand.bias" in keys
+
+
+DFV8_GOLDEN_OPT = {"hidden_dim": 64, "num_heads": 4, "num_bins": 32, "num_aux": 16, "img_size": [64, 96],
+                   "attn_drop_prob": 0.0, "drop_prob": 0.0}
+
+
+def test_state_dict_matches_reference_depthformer_v8():
+    from mdemi.model.Depthformer import DepthformerV8
+    _spec_eq(DepthformerV8(_fake_backend(), DFV8_GOLDEN_OPT, min_depth=1e-3, max_depth=10.0), "depthformer_v8")
+
+
+def test_depthformer_v8_parameter_counts():
+    """Depthformer v8 decoder params 7,167,296 (hidden 256, 4 heads, 256 bins/aux)."""
+    from mdemi.model.Depthformer import DepthformerV8
+    opt = {"hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256, "img_size": [352, 1216]}
+    m = DepthformerV8.build(opt, 1e-3, 80.0)
+    assert sum(p.numel() for p in m.decoder.parameters()) == 7_167_296
+    assert sum(p.numel() for p in m.encoder.parameters()) == 27_288_112  # B5 without conv_head/bn2
