@@ -1,0 +1,66 @@
+"""Per-shape GEMM timing inside one real train step of the bench workload: every libmdemi GEMM
+call is bracketed by HIP events on its stream; calls are grouped by (layouts, ops, M, N, K,
+batch, split) and printed by total time with their TFLOP/s, so the shapes that lose the most
+time against the fp32 MFMA peak stand out.   python tools/gemm_shapes.py [--model newcrfs]"""
+import collections
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "monocular-depth-estimation_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from mdemi import functional as mf  # noqa: E402
+
+
+def main():
+    args = bench.parse()
+    dev = torch.device("cuda", 0)
+    cfg = bench.WORKLOADS[args.model]
+    model, opt, loss_fn = bench.build(args, dev)
+    img, gt = bench.synthetic_batch(cfg["batch"], cfg["h"], cfg["w"], dev, seed=1)
+    for _ in range(2):
+        bench.train_step(model, opt, loss_fn, img, gt)
+    torch.cuda.synchronize()
+    recs = []
+    orig = mf.gemm
+
+    def timed(A, B, C, M, N, K, **kw):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(torch.cuda.current_stream())
+        out = orig(A, B, C, M, N, K, **kw)
+        e.record(torch.cuda.current_stream())
+        split = kw.get("split_k")
+        if split is None:
+            split = mf._split_for(M, N, K)
+        key = (kw.get("a_layout"), kw.get("b_layout"), kw.get("a_op", 0), M, N, K, kw.get("batch", 1), split)
+        recs.append((key, s, e))
+        return out
+
+    mf.gemm = timed
+    try:
+        bench.train_step(model, opt, loss_fn, img, gt)
+        torch.cuda.synchronize()
+    finally:
+        mf.gemm = orig
+    by = collections.defaultdict(lambda: [0.0, 0])
+    for key, s, e in recs:
+        by[key][0] += s.elapsed_time(e) * 1e-3
+        by[key][1] += 1
+    tot_t = sum(v[0] for v in by.values())
+    tot_f = sum(2.0 * k[3] * k[4] * k[5] * k[6] * v[1] for k, v in by.items())
+    print(f"{len(recs)} GEMM calls, {tot_t * 1e3:.2f} ms, {tot_f / tot_t / 1e12:.1f} TF/s")
+    rows = []
+    for k, (t, n) in by.items():
+        fl = 2.0 * k[3] * k[4] * k[5] * k[6] * n
+        lost = t - fl / 157.3e12
+        rows.append((lost, k, t, n, fl / t / 1e12))
+    rows.sort(reverse=True)
+    print("lost_ms  time_ms calls   TF/s  (a_layout,b_layout,a_op,M,N,K,batch,split)")
+    for lost, k, t, n, tf in rows[:45]:
+        print(f"{lost * 1e3:7.2f} {t * 1e3:8.2f} {n:5d} {tf:6.1f}  {k}")
+
+
+if __name__ == "__main__":
+    main()
