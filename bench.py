@@ -42,7 +42,21 @@ WORKLOADS = {
     "newcrfs_kitti": dict(model="NewCRFs-L07", h=352, w=1216, batch=8, max_depth=80.0,
                           workload="NewCRFs Swin-L (large07) train step, KITTI 352x1216",
                           ref_cfg="json/kitti/newcrfs/newcrfs_github_eval.json"),
+    # BASELINE.json configs[1]: AdaBins (EfficientNet-B5 + DecoderBN + mViT + bin head), NYU bs=16;
+    # json/nyu/adabins/adabins_cham_per_batch.json: AdamW lr 3.57e-4 wd 0.1, grad_norm 0.1, SILog a10 b0.15
+    # (its chamfer bin loss, weight 0.1, is not built)
+    "adabins": dict(model="AdaBins-B5", h=480, w=640, batch=16, max_depth=10.0, lr=3.57e-4, wd=0.1, beta=0.15,
+                    per_image=False, workload="AdaBins EfficientNet-B5 train step, NYU 480x640",
+                    ref_cfg="json/nyu/adabins/adabins_cham_per_batch.json"),
+    # Depthformer v8 (json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json model/optimizer
+    # block: hidden 256, 4 heads, 256 bins / aux tokens, lr 3.2e-4 wd 0.1, SILog a10 b0.5 per image) at the
+    # NYU crop, fp32 (BASELINE configs[4]'s bf16 + hipGraph variant is not built)
+    "depthformer": dict(model="DepthformerV8-B5", h=480, w=640, batch=8, max_depth=10.0, lr=3.2e-4, wd=0.1,
+                        beta=0.5, per_image=True, workload="Depthformer v8 train step, NYU 480x640 (fp32)",
+                        ref_cfg="json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json"),
 }
+DFV8_OPT = {"hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256, "img_size": [480, 640],
+            "attn_drop_prob": 0.1, "drop_prob": 0.2}
 # HBM bytes per launch of the roofline kernel family, from the committed
 # rocprofv3 --pmc passes (tools/pmc_traffic.py; FETCH_SIZE doubled per the
 # gfx950 correction).  None when no profile matches the kernel.
@@ -78,20 +92,28 @@ def synthetic_batch(B, H, W, device, seed):
 
 
 def build(args, device):
-    from mdemi.model.NewCRFs import NewCRFDepth
     from mdemi.train import FusedAdamW, SILogLoss
     cfg = WORKLOADS[args.model]
     torch.manual_seed(0)
-    model = NewCRFDepth(version="large07", inv_depth=False, max_depth=cfg["max_depth"]).to(device)
-    model.train()
-    opt = FusedAdamW(model.parameters(), lr=2e-5, weight_decay=0.0, max_grad_norm=0.1)
-    loss_fn = SILogLoss(alpha=10.0, beta=0.15, per_image=False, min_depth=1e-3)
+    if args.model == "adabins":
+        from mdemi.model.Adabins import UnetAdaptiveBins
+        model = UnetAdaptiveBins.build(256, 1e-3, cfg["max_depth"])
+    elif args.model == "depthformer":
+        from mdemi.model.Depthformer import DepthformerV8
+        model = DepthformerV8.build(DFV8_OPT, 1e-3, cfg["max_depth"])
+    else:
+        from mdemi.model.NewCRFs import NewCRFDepth
+        model = NewCRFDepth(version="large07", inv_depth=False, max_depth=cfg["max_depth"])
+    model = model.to(device).train()
+    opt = FusedAdamW(model.parameters(), lr=cfg.get("lr", 2e-5), weight_decay=cfg.get("wd", 0.0), max_grad_norm=0.1)
+    loss_fn = SILogLoss(alpha=10.0, beta=cfg.get("beta", 0.15), per_image=cfg.get("per_image", False), min_depth=1e-3)
     return model, opt, loss_fn
 
 
 def train_step(model, opt, loss_fn, img, gt, ddp=None):
-    pred = model(img)
-    loss = loss_fn(pred, gt)
+    out = model(img)
+    pred = out[0] if isinstance(out, tuple) else out  # AdaBins / Depthformer: (depth at H/2, ...)
+    loss = loss_fn(pred, gt)  # SILogLoss upsamples a half-resolution prediction to the GT first
     loss.backward()
     if ddp is not None:
         ddp.finish()
@@ -150,21 +172,34 @@ def profiled_traffic(regex, workload):
     return ent.get("traffic_bytes_per_launch")
 
 
-def cpu_baseline(model, H, W, budget_s):
-    """The oracle (CPU restatement of the reference path, oracle/newcrfs.py) timed on the host
-    cores: fp32 forward + SILog + backward + AdamW(clip) step at batch 1, same weights."""
+def cpu_baseline(model, name, H, W, budget_s):
+    """The oracle (CPU restatement of the reference path: oracle/newcrfs.py, oracle/adabins.py,
+    oracle/depthformer.py) timed on the host cores: fp32 forward + SILog + backward + clipped AdamW
+    step at batch 1, same weights."""
     from oracle import metrics as omet
-    from oracle import newcrfs as onc
+    cfg = WORKLOADS[name]
     threads = torch.get_num_threads()
     P = {k: v.detach().float().cpu().clone().requires_grad_(torch.is_floating_point(v))
          for k, v in model.state_dict().items()}
     params = [v for v in P.values() if v.requires_grad]
-    opt = torch.optim.AdamW(params, lr=2e-5, weight_decay=0.0)
+    opt = torch.optim.AdamW(params, lr=cfg.get("lr", 2e-5), weight_decay=cfg.get("wd", 0.0))
     img, gt = synthetic_batch(1, H, W, "cpu", seed=1)
+    if name == "adabins":
+        from oracle import adabins as oab
+        fwd = lambda: oab.unet_adaptive_bins(P, img, 1e-3, cfg["max_depth"])[0]  # noqa: E731
+    elif name == "depthformer":
+        from oracle import depthformer as odf
+        opt_m = dict(DFV8_OPT, attn_drop_prob=0.0, drop_prob=0.0)
+        fwd = lambda: odf.depthformer_v8_full(P, img, opt_m, 1e-3, cfg["max_depth"])[0]  # noqa: E731
+    else:
+        from oracle import newcrfs as onc
+        fwd = lambda: onc.newcrf_depth(P, img, "large07", max_depth=cfg["max_depth"])  # noqa: E731
 
     def step():
-        pred = onc.newcrf_depth(P, img, "large07", max_depth=10.0)
-        loss = omet.silog_loss(pred, gt, 1e-3, 10.0, 0.15)
+        pred = fwd()
+        if pred.shape[-2:] != gt.shape[-2:]:
+            pred = torch.nn.functional.interpolate(pred, gt.shape[-2:], mode="bilinear", align_corners=True)
+        loss = omet.silog_loss(pred, gt, 1e-3, 10.0, cfg.get("beta", 0.15), cfg.get("per_image", False))
         loss.backward()
         torch.nn.utils.clip_grad_norm_(params, 0.1)
         opt.step()
@@ -179,7 +214,7 @@ def cpu_baseline(model, H, W, budget_s):
         step()
     dt = (time.perf_counter() - t0) / n
     return {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle NewCRFs-L07 fp32 train step (fwd+SILog+bwd+AdamW), batch 1 at {H}x{W}, "
+            "sample": f"oracle {cfg['model']} fp32 train step (fwd+SILog+bwd+AdamW), batch 1 at {H}x{W}, "
                       f"{n} timed steps after 1 warm-up, {threads} threads, {os.cpu_count()} host CPUs visible"}
 
 
@@ -248,11 +283,12 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(model, H, W, args.cpu_budget_s)
+        cpu = cpu_baseline(model, args.model, H, W, args.cpu_budget_s)
 
     if rank == 0:
         line = {
-            "metric": "images/sec (train step) NYU 640x480 bs=8/GPU",
+            "metric": ("images/sec (train step) NYU 640x480 bs=8/GPU" if args.model == "newcrfs" else
+                       f"images/sec (train step) {cfg['model']} {W}x{H} bs={B}/GPU"),
             "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights)",

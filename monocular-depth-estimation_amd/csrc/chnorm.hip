@@ -189,6 +189,170 @@ __global__ __launch_bounds__(CN_THREADS) void gn_bwd_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// BatchNorm over NHWC with C % 4 == 0 (every BN layer of the hot path): float4
+// channel quads.  A block covers a contiguous run of rows; when C/4 < 256 the
+// block's threads are split into RPT = 256 / (C/4) row lanes that stride the
+// run together (all 256 threads busy for the 24..176-channel EfficientNet
+// maps), partials are combined through LDS and written per block; a second
+// kernel sums the block partials per channel in fp64 (64 channels x 4 lanes per
+// block).  Elementwise passes are float4 with 32-bit quad indices.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float4 f4(float v) { return make_float4(v, v, v, v); }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// PASS 0: sum x; PASS 1: sum (x - mean)^2; PASS 2 (backward): (sum d*xhat, sum d) with
+// d = dy * act'(pre), pre = xhat * gamma + beta recomputed.  part: [blk][NV][C].
+template <int PASS>
+__global__ __launch_bounds__(CN_THREADS) void bn_partial4(const float* __restrict__ x, const float* __restrict__ dy,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ part,
+                                                          int64_t rows, int C, int act, int64_t rows_per_blk) {
+  constexpr int NV = PASS == 2 ? 2 : 1;
+  __shared__ float4 red[NV][CN_THREADS];
+  const int CQ = C >> 2, tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  const int64_t r1 = min(rows, r0 + rows_per_blk);
+  const int rpt = CQ >= CN_THREADS ? 1 : CN_THREADS / CQ;
+  const int lane_r = CQ >= CN_THREADS ? 0 : tid / CQ;
+  for (int cbase = 0; cbase < CQ; cbase += CN_THREADS) {
+    const int c4 = CQ >= CN_THREADS ? cbase + tid : tid % CQ;
+    const bool active = c4 < CQ && lane_r < rpt;
+    float4 s0 = f4(0.f), s1 = f4(0.f);
+    if (active) {
+      const int c = 4 * c4;
+      const float4 mu = PASS ? ld4(mean + c) : f4(0.f);
+      float4 rs = f4(1.f), ga = f4(1.f), be = f4(0.f);
+      if (PASS == 2) { rs = ld4(rstd + c); ga = ld4(gamma + c); be = ld4(beta + c); }
+      for (int64_t r = r0 + lane_r; r < r1; r += rpt) {
+        const float4 v = ld4(x + r * C + c);
+        if (PASS == 0) {
+          s0.x += v.x; s0.y += v.y; s0.z += v.z; s0.w += v.w;
+        } else if (PASS == 1) {
+          const float4 u = make_float4(v.x - mu.x, v.y - mu.y, v.z - mu.z, v.w - mu.w);
+          s0.x = fmaf(u.x, u.x, s0.x); s0.y = fmaf(u.y, u.y, s0.y);
+          s0.z = fmaf(u.z, u.z, s0.z); s0.w = fmaf(u.w, u.w, s0.w);
+        } else {
+          const float4 g = ld4(dy + r * C + c);
+#define MDEMI_BNB(X)                                                  \
+  {                                                                    \
+    const float xh = (v.X - mu.X) * rs.X, pre = xh * ga.X + be.X;      \
+    const float d = g.X * act_grad(act, pre, apply_act(act, pre));     \
+    s0.X = fmaf(d, xh, s0.X);                                          \
+    s1.X += d;                                                         \
+  }
+          MDEMI_BNB(x) MDEMI_BNB(y) MDEMI_BNB(z) MDEMI_BNB(w)
+#undef MDEMI_BNB
+        }
+      }
+    }
+    if (rpt > 1) {  // combine the row lanes of each channel quad
+      red[0][tid] = s0;
+      if (NV == 2) red[NV - 1][tid] = s1;
+      __syncthreads();
+      if (tid < CQ) {
+        for (int k = 1; k < rpt; ++k) {
+          const float4 a = red[0][k * CQ + tid];
+          s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+          if (NV == 2) {
+            const float4 b = red[NV - 1][k * CQ + tid];
+            s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+          }
+        }
+      }
+    }
+    if (rpt > 1 ? tid < CQ : active) {
+      float* dst = part + (int64_t)blockIdx.x * NV * C + 4 * c4;
+      *reinterpret_cast<float4*>(dst) = s0;
+      if (NV == 2) *reinterpret_cast<float4*>(dst + C) = s1;
+    }
+    if (rpt > 1) break;  // one pass covers every quad
+  }
+}
+
+// fp64 sum of the block partials: block = 64 channels x 4 lanes over blocks.
+// MODE 0: mean = s / rows; MODE 1: rstd = 1 / sqrt(s / rows + eps);
+// MODE 2: (dgamma, dbeta) from [blk][2][C].
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_combine4(const float* __restrict__ part, int nblk, int C, int64_t rows,
+                                                   float eps, float* __restrict__ out0, float* __restrict__ out1) {
+  constexpr int NV = MODE == 2 ? 2 : 1;
+  __shared__ double red[NV][4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int i = g; i < nblk; i += 4) {
+      a += (double)part[(int64_t)i * NV * C + c];
+      if (NV == 2) b += (double)part[(int64_t)i * NV * C + C + c];
+    }
+  red[0][g][cl] = a;
+  if (NV == 2) red[NV - 1][g][cl] = b;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    a = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    if (MODE == 0) out0[c] = (float)(a / (double)rows);
+    else if (MODE == 1) out0[c] = (float)(1.0 / sqrt(a / (double)rows + (double)eps));
+    else {
+      b = red[NV - 1][0][cl] + red[NV - 1][1][cl] + red[NV - 1][2][cl] + red[NV - 1][3][cl];
+      out0[c] = (float)a;
+      out1[c] = (float)b;
+    }
+  }
+}
+
+__global__ __launch_bounds__(CN_THREADS) void bn_apply4(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, float* __restrict__ y,
+                                                        int64_t total4, int CQ, int act) {
+  for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
+    const int c = 4 * (int)(e % CQ);
+    const float4 v = reinterpret_cast<const float4*>(x)[e];
+    const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
+    float4 o;
+    o.x = apply_act(act, (v.x - mu.x) * rs.x * ga.x + be.x);
+    o.y = apply_act(act, (v.y - mu.y) * rs.y * ga.y + be.y);
+    o.z = apply_act(act, (v.z - mu.z) * rs.z * ga.z + be.z);
+    o.w = apply_act(act, (v.w - mu.w) * rs.w * ga.w + be.w);
+    reinterpret_cast<float4*>(y)[e] = o;
+  }
+}
+
+__global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply4(const float* __restrict__ dy, const float* __restrict__ x,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            const float* __restrict__ dgamma,
+                                                            const float* __restrict__ dbeta, float* __restrict__ dx,
+                                                            int64_t total4, int CQ, float inv_n, int act) {
+  for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
+    const int c = 4 * (int)(e % CQ);
+    const float4 v = reinterpret_cast<const float4*>(x)[e];
+    const float4 g = reinterpret_cast<const float4*>(dy)[e];
+    const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
+    const float4 dg = ld4(dgamma + c), db = ld4(dbeta + c);
+    float4 o;
+#define MDEMI_BNA(X)                                                                  \
+  {                                                                                    \
+    const float xh = (v.X - mu.X) * rs.X, pre = xh * ga.X + be.X;                      \
+    const float d = g.X * act_grad(act, pre, apply_act(act, pre));                     \
+    o.X = ga.X * rs.X * (d - inv_n * db.X - xh * inv_n * dg.X);                         \
+  }
+    MDEMI_BNA(x) MDEMI_BNA(y) MDEMI_BNA(z) MDEMI_BNA(w)
+#undef MDEMI_BNA
+    reinterpret_cast<float4*>(dx)[e] = o;
+  }
+}
+
+// blocks for the vectorised path: enough to fill the chip, >= 16 rows each
+static int bn4_blocks(int64_t rows) {
+  int64_t nb = cdiv(rows, 16);
+  return (int)(nb > 2048 ? 2048 : (nb < 1 ? 1 : nb));
+}
+
 static int rows_per_block(int64_t rows) {
   // ~256 partial blocks
   int64_t rpb = cdiv(rows, 256);
@@ -208,7 +372,8 @@ extern "C" size_t mdemi_chnorm_workspace_size(int32_t N, int64_t HW, int32_t C, 
   if (is_bn) {
     const int64_t rows = (int64_t)N * HW;
     const int64_t nblk = cdiv(rows, rows_per_block(rows));
-    return (size_t)nblk * 2 * C * sizeof(float);
+    const int64_t nb4 = bn4_blocks(rows);
+    return (size_t)(nblk > nb4 ? nblk : nb4) * 2 * C * sizeof(float);
   }
   return (size_t)N * 2 * C * sizeof(float);
 }
@@ -221,9 +386,24 @@ extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float*
   if (is_bn) {
     if (!workspace) { set_error("chnorm_fwd: workspace required"); return MDEMI_EWORKSPACE; }
     const int64_t rows = (int64_t)N * HW;
+    float* part = (float*)workspace;
+    if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+      const int nb = bn4_blocks(rows);
+      const int64_t rpb4 = cdiv(rows, nb);
+      const unsigned cg = (unsigned)cdiv(C, 64);
+      hipLaunchKernelGGL(bn_partial4<0>, dim3(nb), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma, beta, part,
+                         rows, C, act, rpb4);
+      hipLaunchKernelGGL(bn_combine4<0>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, mean, nullptr);
+      hipLaunchKernelGGL(bn_partial4<1>, dim3(nb), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma, beta, part,
+                         rows, C, act, rpb4);
+      hipLaunchKernelGGL(bn_combine4<1>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, rstd, nullptr);
+      const int64_t total4 = rows * C / 4;
+      hipLaunchKernelGGL(bn_apply4, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, x, gamma, beta, mean, rstd, y,
+                         total4, C / 4, act);
+      return check_launch("chnorm_fwd");
+    }
     const int rpb = rows_per_block(rows);
     const int nblk = (int)cdiv(rows, rpb);
-    float* part = (float*)workspace;
     hipLaunchKernelGGL(bn_partial, dim3(nblk), dim3(CN_THREADS), 0, st, x, mean, part, rows, C, 0, rpb);
     hipLaunchKernelGGL(bn_combine, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, rows, 0, eps, mean, rstd);
     hipLaunchKernelGGL(bn_partial, dim3(nblk), dim3(CN_THREADS), 0, st, x, mean, part, rows, C, 1, rpb);
@@ -263,6 +443,18 @@ extern "C" int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y,
   float* part = (float*)workspace;
   if (is_bn) {
     const int64_t rows = (int64_t)N * HW;
+    if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
+      const int nb = bn4_blocks(rows);
+      const int64_t rpb4 = cdiv(rows, nb);
+      hipLaunchKernelGGL(bn_partial4<2>, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta, part, rows,
+                         C, act, rpb4);
+      hipLaunchKernelGGL(bn_combine4<2>, dim3((unsigned)cdiv(C, 64)), dim3(256), 0, st, part, nb, C, rows, 0.f, dgamma,
+                         dbeta);
+      const int64_t total4 = rows * C / 4;
+      hipLaunchKernelGGL(bn_bwd_apply4, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma, beta,
+                         dgamma, dbeta, dx, total4, C / 4, 1.f / (float)rows, act);
+      return check_launch("chnorm_bwd");
+    }
     const int rpb = rows_per_block(rows);
     const int nblk = (int)cdiv(rows, rpb);
     hipLaunchKernelGGL(bn_bwd_partial, dim3(nblk), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma, beta, part, rows,

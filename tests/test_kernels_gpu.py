@@ -318,6 +318,30 @@ def test_channel_norm(mf, is_bn, groups, act):
     close(bg.grad, br.grad, rtol=1e-4)
 
 
+@pytest.mark.parametrize("n,c,h,w,act", [(2, 48, 120, 160, 6), (2, 600, 9, 11, 3), (1, 1100, 7, 9, 0),
+                                         (3, 6, 10, 10, 2), (4, 24, 1, 1, 6), (2, 2048, 15, 20, 3)])
+def test_batch_norm_shapes(mf, n, c, h, w, act):
+    """Training BatchNorm + fused activation over NHWC: the vectorised path (C % 4 == 0) with
+    many row lanes per channel quad (C=48, 24), one lane with idle threads (C=600), several quad
+    passes per block (C=1100, 2048), and the scalar path (C=6)."""
+    from mdemi import _lib as L
+    x = rnd(n, c, h, w, seed=64, scale=3) + 1
+    g, b = rnd(c, seed=65), rnd(c, seed=66)
+    dy = rnd(n, c, h, w, seed=67)
+    xr, gr, br = [t.clone().requires_grad_() for t in (x, g, b)]
+    yr = F.batch_norm(xr, None, None, gr, br, training=True, eps=1e-3)
+    yr = {L.ACT_RELU: F.relu, L.ACT_SILU: F.silu, L.ACT_LEAKY: F.leaky_relu, L.ACT_NONE: lambda t: t}[act](yr)
+    yr.backward(dy)
+    xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV).requires_grad_()
+    gg, bg = g.float().to(DEV).requires_grad_(), b.float().to(DEV).requires_grad_()
+    yg, _, _ = mf.batch_norm_nhwc(xg, gg, bg, 1e-3, act)
+    yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+    close(yg.permute(0, 3, 1, 2), yr, rtol=1e-5)
+    close(xg.grad.permute(0, 3, 1, 2), xr.grad, rtol=1e-4)
+    close(gg.grad, gr.grad, rtol=1e-4)
+    close(bg.grad, br.grad, rtol=1e-4)
+
+
 def test_pixel_shuffle_avgpool_patch(mf):
     n, c, h, w = 2, 16, 5, 7
     x = rnd(n, c, h, w, seed=70)
