@@ -272,31 +272,38 @@ __global__ __launch_bounds__(CN_THREADS) void bn_partial4(const float* __restric
   }
 }
 
-// fp64 sum of the block partials: block = 64 channels x 4 lanes over blocks.
+// fp64 sum of the block partials: a block owns CPB = min(C, 64) channels and
+// splits the partial rows over 256 / CPB lanes per channel (so narrow layers
+// still use the whole block), then folds the lanes through LDS.
 // MODE 0: mean = s / rows; MODE 1: rstd = 1 / sqrt(s / rows + eps);
 // MODE 2: (dgamma, dbeta) from [blk][2][C].
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_combine4(const float* __restrict__ part, int nblk, int C, int64_t rows,
                                                    float eps, float* __restrict__ out0, float* __restrict__ out1) {
   constexpr int NV = MODE == 2 ? 2 : 1;
-  __shared__ double red[NV][4][64];
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ double red[NV][256];
+  const int cpb = C < 64 ? C : 64, lpc = 256 / cpb;
+  const int cl = threadIdx.x % cpb, g = threadIdx.x / cpb;
+  const int c = blockIdx.x * cpb + cl;
   double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int i = g; i < nblk; i += 4) {
+  if (c < C && g < lpc)
+    for (int i = g; i < nblk; i += lpc) {
       a += (double)part[(int64_t)i * NV * C + c];
       if (NV == 2) b += (double)part[(int64_t)i * NV * C + C + c];
     }
-  red[0][g][cl] = a;
-  if (NV == 2) red[NV - 1][g][cl] = b;
+  red[0][threadIdx.x] = a;
+  if (NV == 2) red[NV - 1][threadIdx.x] = b;
   __syncthreads();
   if (g == 0 && c < C) {
-    a = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    a = 0.0;
+    b = 0.0;
+    for (int k = 0; k < lpc; ++k) {
+      a += red[0][k * cpb + cl];
+      if (NV == 2) b += red[NV - 1][k * cpb + cl];
+    }
     if (MODE == 0) out0[c] = (float)(a / (double)rows);
     else if (MODE == 1) out0[c] = (float)(1.0 / sqrt(a / (double)rows + (double)eps));
     else {
-      b = red[NV - 1][0][cl] + red[NV - 1][1][cl] + red[NV - 1][2][cl] + red[NV - 1][3][cl];
       out0[c] = (float)a;
       out1[c] = (float)b;
     }
@@ -350,8 +357,9 @@ __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply4(const float* __restr
 // blocks for the vectorised path: enough to fill the chip, >= 16 rows each
 static int bn4_blocks(int64_t rows) {
   int64_t nb = cdiv(rows, 16);
-  return (int)(nb > 2048 ? 2048 : (nb < 1 ? 1 : nb));
+  return (int)(nb > 1024 ? 1024 : (nb < 1 ? 1 : nb));
 }
+static unsigned bn4_combine_grid(int C) { return (unsigned)cdiv(C, C < 64 ? C : 64); }
 
 static int rows_per_block(int64_t rows) {
   // ~256 partial blocks
@@ -390,7 +398,7 @@ extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float*
     if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
       const int nb = bn4_blocks(rows);
       const int64_t rpb4 = cdiv(rows, nb);
-      const unsigned cg = (unsigned)cdiv(C, 64);
+      const unsigned cg = bn4_combine_grid(C);
       hipLaunchKernelGGL(bn_partial4<0>, dim3(nb), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma, beta, part,
                          rows, C, act, rpb4);
       hipLaunchKernelGGL(bn_combine4<0>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, mean, nullptr);
@@ -448,7 +456,7 @@ extern "C" int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y,
       const int64_t rpb4 = cdiv(rows, nb);
       hipLaunchKernelGGL(bn_partial4<2>, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta, part, rows,
                          C, act, rpb4);
-      hipLaunchKernelGGL(bn_combine4<2>, dim3((unsigned)cdiv(C, 64)), dim3(256), 0, st, part, nb, C, rows, 0.f, dgamma,
+      hipLaunchKernelGGL(bn_combine4<2>, dim3(bn4_combine_grid(C)), dim3(256), 0, st, part, nb, C, rows, 0.f, dgamma,
                          dbeta);
       const int64_t total4 = rows * C / 4;
       hipLaunchKernelGGL(bn_bwd_apply4, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma, beta,
@@ -482,4 +490,24 @@ extern "C" int mdemi_chnorm_apply(const float* x, const float* gamma, const floa
   hipLaunchKernelGGL(chnorm_apply, dim3(grid_for((int64_t)N * HW * C)), dim3(CN_THREADS), 0, (hipStream_t)stream, x,
                      gamma, beta, mean, rstd, y, N, HW, C, G, is_bn, act);
   return check_launch("chnorm_apply");
+}
+
+__global__ void bn_running_kernel(const float* __restrict__ mean, const float* __restrict__ rstd,
+                                  float* __restrict__ rmean, float* __restrict__ rvar, int C, float unbias, float eps,
+                                  float m) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float r = rstd[c];
+  const float var = (1.f / (r * r) - eps) * unbias;
+  rmean[c] = (1.f - m) * rmean[c] + m * mean[c];
+  rvar[c] = (1.f - m) * rvar[c] + m * var;
+}
+
+extern "C" int mdemi_bn_running_update(const float* mean, const float* rstd, float* running_mean, float* running_var,
+                                       int32_t C, int64_t rows, float eps, float momentum, void* stream) {
+  MDEMI_REQUIRE(mean && rstd && running_mean && running_var && C > 0 && rows > 0, "bn_running_update: bad args");
+  const float unbias = (float)((double)rows / (double)(rows > 1 ? rows - 1 : 1));
+  hipLaunchKernelGGL(bn_running_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, mean, rstd,
+                     running_mean, running_var, C, unbias, eps, momentum);
+  return check_launch("bn_running_update");
 }

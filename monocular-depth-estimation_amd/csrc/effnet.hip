@@ -283,70 +283,74 @@ __global__ __launch_bounds__(256) void chan_scale_kernel(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// SqueezeExcite gate MLP: one block per image.
+// SqueezeExcite gate MLP, split so that every stage has N x (R/4 or C/256)
+// workgroups (one workgroup per image left 240 of 256 CUs idle at batch 16):
+//   hid[n][r]  = br[r] + sum_c wr[r][c] pooled[n][c]        (wave per (n, r))
+//   gate[n][c] = sigmoid(be[c] + sum_r we[c][r] silu(hid[n][r]))   (thread per (n, c))
 // ---------------------------------------------------------------------------
 constexpr int SE_MAXC = 4096, SE_MAXR = 256;
 
-__global__ __launch_bounds__(256) void se_gate_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ wr,
-                                                          const float* __restrict__ br, const float* __restrict__ we,
-                                                          const float* __restrict__ be, float* __restrict__ hid,
-                                                          float* __restrict__ gate, int C, int R) {
-  __shared__ float sp[SE_MAXC];
-  __shared__ float sh[SE_MAXR];
-  const int n = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int c = threadIdx.x; c < C; c += 256) sp[c] = pooled[(int64_t)n * C + c];
-  __syncthreads();
-  for (int r = wid; r < R; r += 4) {
-    const float* wrow = wr + (int64_t)r * C;
-    float s = 0.f;
-    for (int c = lane; c < C; c += 64) s = fmaf(wrow[c], sp[c], s);
-    s = wave_sum(s) + br[r];
-    if (lane == 0) {
-      hid[(int64_t)n * R + r] = s;
-      sh[r] = silu_f(s);
-    }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const float* wrow = we + (int64_t)c * R;
-    float s = be[c];
-    for (int r = 0; r < R; ++r) s = fmaf(wrow[r], sh[r], s);
-    gate[(int64_t)n * C + c] = sigmoid_f(s);
-  }
+__global__ __launch_bounds__(256) void se_hid_kernel(const float* __restrict__ pooled, const float* __restrict__ wr,
+                                                     const float* __restrict__ br, float* __restrict__ hid, int C,
+                                                     int R) {
+  const int n = blockIdx.x, lane = threadIdx.x & 63;
+  const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* wrow = wr + (int64_t)r * C;
+  const float* pv = pooled + (int64_t)n * C;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s = fmaf(wrow[c], pv[c], s);
+  s = wave_sum(s);
+  if (lane == 0) hid[(int64_t)n * R + r] = s + br[r];
 }
 
-// per image: de = dgate * g(1-g); dz = (we^T de) * silu'(hid); dpooled = wr^T dz
-__global__ __launch_bounds__(256) void se_gate_bwd_kernel(const float* __restrict__ wr, const float* __restrict__ we,
-                                                          const float* __restrict__ hid, const float* __restrict__ gate,
-                                                          const float* __restrict__ dgate, float* __restrict__ dpooled,
-                                                          float* __restrict__ de_out, float* __restrict__ dz_out, int C,
-                                                          int R) {
-  __shared__ float sde[SE_MAXC];
+__global__ __launch_bounds__(256) void se_gate_kernel(const float* __restrict__ hid, const float* __restrict__ we,
+                                                      const float* __restrict__ be, float* __restrict__ gate, int C,
+                                                      int R) {
+  __shared__ float sh[SE_MAXR];
+  const int n = blockIdx.x;
+  for (int r = threadIdx.x; r < R; r += 256) sh[r] = silu_f(hid[(int64_t)n * R + r]);
+  __syncthreads();
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* wrow = we + (int64_t)c * R;
+  float s = be[c];
+  for (int r = 0; r < R; ++r) s = fmaf(wrow[r], sh[r], s);
+  gate[(int64_t)n * C + c] = sigmoid_f(s);
+}
+
+// backward, per image: de = dgate * g(1-g); dz = (we^T de) * silu'(hid); dpooled = wr^T dz
+__global__ __launch_bounds__(256) void se_dz_kernel(const float* __restrict__ we, const float* __restrict__ hid,
+                                                    const float* __restrict__ gate, const float* __restrict__ dgate,
+                                                    float* __restrict__ de_out, float* __restrict__ dz_out, int C,
+                                                    int R) {
+  const int n = blockIdx.x, lane = threadIdx.x & 63;
+  const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const float* gv = gate + (int64_t)n * C;
+  const float* dgv = dgate + (int64_t)n * C;
+  if (blockIdx.y == 0)  // de is also the conv_expand bias/weight gradient's input
+    for (int c = threadIdx.x; c < C; c += 256) de_out[(int64_t)n * C + c] = dgv[c] * gv[c] * (1.f - gv[c]);
+  if (r >= R) return;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float g = gv[c];
+    s = fmaf(we[(int64_t)c * R + r], dgv[c] * g * (1.f - g), s);
+  }
+  s = wave_sum(s);
+  if (lane == 0) dz_out[(int64_t)n * R + r] = s * silu_grad_f(hid[(int64_t)n * R + r]);
+}
+
+__global__ __launch_bounds__(256) void se_dpooled_kernel(const float* __restrict__ wr, const float* __restrict__ dz,
+                                                         float* __restrict__ dpooled, int C, int R) {
   __shared__ float sdz[SE_MAXR];
-  const int n = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const float g = gate[(int64_t)n * C + c];
-    const float d = dgate[(int64_t)n * C + c] * g * (1.f - g);
-    sde[c] = d;
-    de_out[(int64_t)n * C + c] = d;
-  }
+  const int n = blockIdx.x;
+  for (int r = threadIdx.x; r < R; r += 256) sdz[r] = dz[(int64_t)n * R + r];
   __syncthreads();
-  for (int r = wid; r < R; r += 4) {
-    float s = 0.f;
-    for (int c = lane; c < C; c += 64) s = fmaf(we[(int64_t)c * R + r], sde[c], s);
-    s = wave_sum(s);
-    if (lane == 0) {
-      const float dz = s * silu_grad_f(hid[(int64_t)n * R + r]);
-      sdz[r] = dz;
-      dz_out[(int64_t)n * R + r] = dz;
-    }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f;
-    for (int r = 0; r < R; ++r) s = fmaf(wr[(int64_t)r * C + c], sdz[r], s);
-    dpooled[(int64_t)n * C + c] = s;
-  }
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s = fmaf(wr[(int64_t)r * C + c], sdz[r], s);
+  dpooled[(int64_t)n * C + c] = s;
 }
 
 // parameter gradients, summed over the N images in order
@@ -503,8 +507,9 @@ extern "C" int mdemi_se_gate_fwd(const float* pooled, const float* wr, const flo
                                  void* stream) {
   MDEMI_REQUIRE(pooled && wr && br && we && be && hid && gate && N > 0 && C > 0 && R > 0, "se_gate_fwd: bad args");
   MDEMI_REQUIRE(C <= SE_MAXC && R <= SE_MAXR, "se_gate_fwd: C=%d R=%d exceed %d/%d", C, R, SE_MAXC, SE_MAXR);
-  hipLaunchKernelGGL(se_gate_fwd_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, pooled, wr, br, we, be, hid,
-                     gate, C, R);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(se_hid_kernel, dim3(N, (unsigned)cdiv(R, 4)), dim3(256), 0, st, pooled, wr, br, hid, C, R);
+  hipLaunchKernelGGL(se_gate_kernel, dim3(N, (unsigned)cdiv(C, 256)), dim3(256), 0, st, hid, we, be, gate, C, R);
   return check_launch("se_gate_fwd");
 }
 
@@ -523,7 +528,8 @@ extern "C" int mdemi_se_gate_bwd(const float* pooled, const float* wr, const flo
   float* de = (float*)workspace;
   float* dz = de + (int64_t)N * C;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(se_gate_bwd_kernel, dim3(N), dim3(256), 0, st, wr, we, hid, gate, dgate, dpooled, de, dz, C, R);
+  hipLaunchKernelGGL(se_dz_kernel, dim3(N, (unsigned)cdiv(R, 4)), dim3(256), 0, st, we, hid, gate, dgate, de, dz, C, R);
+  hipLaunchKernelGGL(se_dpooled_kernel, dim3(N, (unsigned)cdiv(C, 256)), dim3(256), 0, st, wr, dz, dpooled, C, R);
   const int64_t total = 2 * (int64_t)R * C + C + R;
   hipLaunchKernelGGL(se_gate_wgrad_kernel, dim3(grid_1d(total)), dim3(256), 0, st, pooled, hid, de, dz, dwr, dbr, dwe,
                      dbe, N, C, R);

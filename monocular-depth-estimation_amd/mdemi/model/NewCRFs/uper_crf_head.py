@@ -55,11 +55,13 @@ def bn_forward(bn: nn.BatchNorm2d, x, act=L.ACT_NONE):
         if bn.track_running_stats:
             with torch.no_grad():
                 n = x.numel() // x.shape[-1]
-                var = (1.0 / (rstd * rstd) - bn.eps) * (n / max(n - 1, 1))
                 bn.num_batches_tracked.add_(1)
-                m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
-                bn.running_mean.mul_(1 - m).add_(mean, alpha=m)
-                bn.running_var.mul_(1 - m).add_(var, alpha=m)
+                if bn.momentum is None:  # cumulative average: needs the count on the host
+                    m = 1.0 / float(bn.num_batches_tracked)
+                else:
+                    m = bn.momentum
+                L.call("mdemi_bn_running_update", mean.data_ptr(), rstd.data_ptr(), bn.running_mean.data_ptr(),
+                       bn.running_var.data_ptr(), x.shape[-1], n, float(bn.eps), float(m), L.stream())
         return y
     return mf.batch_norm_eval_nhwc(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, act)
 

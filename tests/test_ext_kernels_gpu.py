@@ -71,8 +71,8 @@ def test_dwconv_same(mf, k, s, hw, c):
     close(wg.grad, wr.grad, rtol=1e-5 * math.sqrt(n_acc))
 
 
-def test_squeeze_excite(mf):
-    n, c, r, h, w = 3, 48, 12, 7, 9
+@pytest.mark.parametrize("n,c,r,h,w", [(3, 48, 12, 7, 9), (2, 600, 26, 5, 6), (2, 3072, 128, 2, 3)])
+def test_squeeze_excite(mf, n, c, r, h, w):
     x, wr, br = rnd(n, c, h, w, seed=4, scale=2), rnd(r, c, seed=5, scale=0.3), rnd(r, seed=6)
     we, be = rnd(c, r, seed=7, scale=0.3), rnd(c, seed=8)
     ts = [t.clone().requires_grad_() for t in (x, wr, br, we, be)]

@@ -342,6 +342,24 @@ def test_batch_norm_shapes(mf, n, c, h, w, act):
     close(bg.grad, br.grad, rtol=1e-4)
 
 
+@pytest.mark.parametrize("momentum", [0.1, None])
+def test_batch_norm_running_stats(mf, momentum):
+    """bn_forward (the model-side BatchNorm2d) updates running_mean / running_var / the batch
+    counter exactly as nn.BatchNorm2d does in training (unbiased variance, momentum or
+    cumulative average), through mdemi_bn_running_update."""
+    from mdemi.model.NewCRFs.uper_crf_head import bn_forward
+    c = 40
+    ref = torch.nn.BatchNorm2d(c, eps=1e-3, momentum=momentum).double()
+    bn = torch.nn.BatchNorm2d(c, eps=1e-3, momentum=momentum).to(DEV)
+    for step in range(3):
+        x = rnd(2, c, 5, 7, seed=90 + step, scale=2) + 0.5
+        ref(x)
+        bn_forward(bn, x.permute(0, 2, 3, 1).contiguous().float().to(DEV))
+    close(bn.running_mean, ref.running_mean, rtol=1e-5, atol=1e-6)
+    close(bn.running_var, ref.running_var, rtol=1e-5, atol=1e-6)
+    assert int(bn.num_batches_tracked) == 3
+
+
 def test_pixel_shuffle_avgpool_patch(mf):
     n, c, h, w = 2, 16, 5, 7
     x = rnd(n, c, h, w, seed=70)
