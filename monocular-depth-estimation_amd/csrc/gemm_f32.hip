@@ -757,6 +757,15 @@ static size_t rowsum_bytes(const mdemi_gemm_desc* d, const GemmParams& p) {
   return (p.split > 1 && d->rowsum_a) ? (size_t)p.split * d->M * sizeof(float) : 0;
 }
 
+// split-K combine by column sums: deep splits with a plain store epilogue
+static bool colsum_combine(const mdemi_gemm_desc* d, const GemmParams& p) {
+  return p.split >= 32 && d->batch == 1 && d->alpha == 1.f && d->beta == 0.f && d->bias_mode == MDEMI_BIAS_NONE &&
+         d->act == MDEMI_ACT_NONE && !d->residual && !d->preact && d->ldc == d->N;
+}
+static size_t colsum_combine_bytes(const mdemi_gemm_desc* d, const GemmParams& p) {
+  return colsum_combine(d, p) ? colsum_ws_bytes(p.split, (int64_t)d->M * d->N) : 0;
+}
+
 static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
   KernelFn fn = pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant);
   if (!fn) {
@@ -768,7 +777,7 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
   fill_params(d, p, variant);
   float* rowsum_part = nullptr;
   if (p.split > 1) {
-    const size_t need = slab_bytes(d, p) + rowsum_bytes(d, p);
+    const size_t need = slab_bytes(d, p) + rowsum_bytes(d, p) + colsum_combine_bytes(d, p);
     if (!d->workspace || (size_t)d->workspace_bytes < need) {
       set_error("gemm: split-K needs %zu workspace bytes", need);
       return MDEMI_EWORKSPACE;
@@ -783,10 +792,20 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
   MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
   hipLaunchKernelGGL(fn, dim3((unsigned)nblocks), dim3(GTHREADS), 0, st, p);
   if (p.split > 1) {
-    const int64_t total = (int64_t)d->M * d->N * d->batch / ((d->N & 3) == 0 ? 4 : 1);
-    const int nb = (int)(cdiv(total, 256) < 4096 ? cdiv(total, 256) : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(nb), dim3(256), 0, st, p, (const float*)rowsum_part,
-                       rowsum_part ? d->rowsum_a : (float*)nullptr);
+    if (colsum_combine(d, p)) {
+      // many slabs over a small C (skinny weight gradients over ~10^6 pixels): a
+      // column sum parallel over the slab rows, not one thread per output summing
+      // `split` dependent loads
+      char* cws = (char*)d->workspace + slab_bytes(d, p) + rowsum_bytes(d, p);
+      int rc = colsum_launch(p.slab, p.split, (int64_t)d->M * d->N, (int64_t)d->M * d->N, d->C, 0, cws, st);
+      if (!rc && rowsum_part) rc = colsum_launch(rowsum_part, p.split, d->M, d->M, d->rowsum_a, 0, cws, st);
+      if (rc) return rc;
+    } else {
+      const int64_t total = (int64_t)d->M * d->N * d->batch / ((d->N & 3) == 0 ? 4 : 1);
+      const int nb = (int)(cdiv(total, 256) < 4096 ? cdiv(total, 256) : 4096);
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3(nb), dim3(256), 0, st, p, (const float*)rowsum_part,
+                         rowsum_part ? d->rowsum_a : (float*)nullptr);
+    }
   }
   return check_launch("gemm_f32");
 }
@@ -847,7 +866,7 @@ extern "C" size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d) {
   GemmParams p;
   fill_params(d, p, 0);  // the split count does not depend on the variant
   if (p.split <= 1) return 0;
-  return slab_bytes(d, p) + rowsum_bytes(d, p);
+  return slab_bytes(d, p) + rowsum_bytes(d, p) + colsum_combine_bytes(d, p);
 }
 
 extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {

@@ -36,12 +36,15 @@ def _target_blocks():
 
 
 def _split_for(M, N, K):
-    """Split-K factor so that a long reduction still fills the chip."""
+    """Split-K factor so that a long reduction still fills the chip.  Skinny outputs (fewer
+    than 8 tiles: the weight gradients of narrow 1x1 convs over ~10^6 pixels) split up to 512
+    ways (each split still >= 256 rows of K); their slabs are combined by a column sum."""
     tiles = math.ceil(M / 128) * math.ceil(N / 128)
     ktiles = math.ceil(K / 16)
     if tiles >= 512 or ktiles < 32:
         return 1
-    split = min(max(1, _target_blocks() // tiles), ktiles // 16, 64)
+    target, cap = (_target_blocks(), 64) if tiles >= 8 else (2 * _target_blocks(), 512)
+    split = min(max(1, target // tiles), ktiles // 16, cap)
     return max(1, split)
 
 

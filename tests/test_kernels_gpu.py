@@ -464,6 +464,22 @@ def test_space_to_depth_concat_droppath(mf):
     close(y, exp.cpu(), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("M,N,K", [(24, 40, 300000), (144, 24, 123457), (240, 40, 70000)])
+def test_gemm_deep_split_skinny_wgrad(mf, M, N, K):
+    """Weight gradient of a narrow 1x1 conv over many pixels (dW = dY^T X, db = dY^T 1): deep
+    split-K (up to 512 slabs) combined by column sums, with the bias row-sum folded in."""
+    from mdemi import _lib as L
+    split = mf._split_for(M, N, K)
+    assert split >= 32
+    dy = torch.randn(K, M, device=DEV)
+    x = torch.randn(K, N, device=DEV)
+    dw = torch.empty(M, N, device=DEV)
+    db = torch.empty(M, device=DEV)
+    mf.gemm(dy, x, dw, M, N, K, lda=M, ldb=N, ldc=N, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG, rowsum_a=db)
+    close(dw, (dy.double().t() @ x.double()).cpu(), rtol=2e-6 * math.sqrt(K))
+    close(db, dy.double().sum(0).cpu(), rtol=2e-6 * math.sqrt(K))
+
+
 @pytest.mark.parametrize("layouts", ["fwd", "dgrad", "wgrad"])
 def test_gemm_variants_bit_identical(mf, layouts):
     """Every pipelining variant (and hence the per-shape autotuner's pick) adds
