@@ -272,9 +272,10 @@ __global__ __launch_bounds__(CN_THREADS) void bn_partial4(const float* __restric
   }
 }
 
-// fp64 sum of the block partials: a block owns CPB = min(C, 64) channels and
-// splits the partial rows over 256 / CPB lanes per channel (so narrow layers
-// still use the whole block), then folds the lanes through LDS.
+// fp64 sum of the block partials: a block owns CPB = min(C, 16) channels and
+// splits the partial rows over 256 / CPB lanes per channel, each lane keeping
+// four independent accumulators (memory-level parallelism over the strided
+// partial rows), then folds lanes and accumulators in a fixed order.
 // MODE 0: mean = s / rows; MODE 1: rstd = 1 / sqrt(s / rows + eps);
 // MODE 2: (dgamma, dbeta) from [blk][2][C].
 template <int MODE>
@@ -282,30 +283,39 @@ __global__ __launch_bounds__(256) void bn_combine4(const float* __restrict__ par
                                                    float eps, float* __restrict__ out0, float* __restrict__ out1) {
   constexpr int NV = MODE == 2 ? 2 : 1;
   __shared__ double red[NV][256];
-  const int cpb = C < 64 ? C : 64, lpc = 256 / cpb;
+  const int cpb = C < 16 ? C : 16, lpc = 256 / cpb;
   const int cl = threadIdx.x % cpb, g = threadIdx.x / cpb;
   const int c = blockIdx.x * cpb + cl;
-  double a = 0.0, b = 0.0;
-  if (c < C && g < lpc)
-    for (int i = g; i < nblk; i += lpc) {
-      a += (double)part[(int64_t)i * NV * C + c];
-      if (NV == 2) b += (double)part[(int64_t)i * NV * C + C + c];
+  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C && g < lpc) {
+    const int64_t stride = (int64_t)NV * C;
+    int i = g;
+    for (; i + 3 * lpc < nblk; i += 4 * lpc) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] += (double)part[(int64_t)(i + u * lpc) * stride + c];
+        if (NV == 2) b[u] += (double)part[(int64_t)(i + u * lpc) * stride + C + c];
+      }
     }
-  red[0][threadIdx.x] = a;
-  if (NV == 2) red[NV - 1][threadIdx.x] = b;
+    for (; i < nblk; i += lpc) {
+      a[0] += (double)part[(int64_t)i * stride + c];
+      if (NV == 2) b[0] += (double)part[(int64_t)i * stride + C + c];
+    }
+  }
+  red[0][threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
+  if (NV == 2) red[NV - 1][threadIdx.x] = (b[0] + b[1]) + (b[2] + b[3]);
   __syncthreads();
   if (g == 0 && c < C) {
-    a = 0.0;
-    b = 0.0;
+    double sa = 0.0, sb = 0.0;
     for (int k = 0; k < lpc; ++k) {
-      a += red[0][k * cpb + cl];
-      if (NV == 2) b += red[NV - 1][k * cpb + cl];
+      sa += red[0][k * cpb + cl];
+      if (NV == 2) sb += red[NV - 1][k * cpb + cl];
     }
-    if (MODE == 0) out0[c] = (float)(a / (double)rows);
-    else if (MODE == 1) out0[c] = (float)(1.0 / sqrt(a / (double)rows + (double)eps));
+    if (MODE == 0) out0[c] = (float)(sa / (double)rows);
+    else if (MODE == 1) out0[c] = (float)(1.0 / sqrt(sa / (double)rows + (double)eps));
     else {
-      out0[c] = (float)a;
-      out1[c] = (float)b;
+      out0[c] = (float)sa;
+      out1[c] = (float)sb;
     }
   }
 }
@@ -359,7 +369,7 @@ static int bn4_blocks(int64_t rows) {
   int64_t nb = cdiv(rows, 16);
   return (int)(nb > 1024 ? 1024 : (nb < 1 ? 1 : nb));
 }
-static unsigned bn4_combine_grid(int C) { return (unsigned)cdiv(C, C < 64 ? C : 64); }
+static unsigned bn4_combine_grid(int C) { return (unsigned)cdiv(C, C < 16 ? C : 16); }
 
 static int rows_per_block(int64_t rows) {
   // ~256 partial blocks
