@@ -129,6 +129,64 @@ __global__ __launch_bounds__(256) void dwconv_dx_kernel(const float* __restrict_
   }
 }
 
+// stride-1 input gradient as a row sweep (the correlation of dy with the
+// flipped taps): the TX outputs of a thread share one pass over the TX+K-1
+// dy columns of each tap row, instead of K*K*TX separate loads.
+template <int K, int TX>
+__global__ __launch_bounds__(256) void dwconv_dx_s1_kernel(const float* __restrict__ dy, const float* __restrict__ w,
+                                                           float* __restrict__ dx, int N, int H, int W, int C,
+                                                           int pad_t, int pad_l, int OH, int OW) {
+  constexpr int KK = K * K, SPAN = TX + K - 1;
+  const int C4 = C >> 2, WT = (W + TX - 1) / TX;
+  const int64_t total = (int64_t)N * H * WT * C4;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c4 = (int)(e % C4);
+    int64_t t = e / C4;
+    const int ixt = (int)(t % WT); t /= WT;
+    const int iy = (int)(t % H);
+    const int n = (int)(t / H);
+    const int c = c4 * 4;
+    const int ix0 = ixt * TX;
+    // output columns ox = ix + pad_l - kx; the sweep starts at ix0 + pad_l - (K-1)
+    const int ox0 = ix0 + pad_l - (K - 1);
+    float4 acc[TX];
+#pragma unroll
+    for (int q = 0; q < TX; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* w0 = w + (int64_t)c * KK;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int oy = iy + pad_t - ky;
+      if (oy < 0 || oy >= OH) continue;
+      float4 wk[K];
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx)
+        wk[kx] = make_float4(w0[ky * K + kx], w0[KK + ky * K + kx], w0[2 * KK + ky * K + kx],
+                             w0[3 * KK + ky * K + kx]);
+      const float* row = dy + (((int64_t)n * OH + oy) * OW) * C + c;
+#pragma unroll
+      for (int j = 0; j < SPAN; ++j) {
+        const int ox = ox0 + j;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ox >= 0 && ox < OW) v = *reinterpret_cast<const float4*>(row + (int64_t)ox * C);
+#pragma unroll
+        for (int q = 0; q < TX; ++q) {
+          const int kx = q + (K - 1) - j;  // ox = ix0 + q + pad_l - kx
+          if (kx >= 0 && kx < K) {
+            acc[q].x = fmaf(v.x, wk[kx].x, acc[q].x);
+            acc[q].y = fmaf(v.y, wk[kx].y, acc[q].y);
+            acc[q].z = fmaf(v.z, wk[kx].z, acc[q].z);
+            acc[q].w = fmaf(v.w, wk[kx].w, acc[q].w);
+          }
+        }
+      }
+    }
+    float* out = dx + (((int64_t)n * H + iy) * W) * C + c;
+#pragma unroll
+    for (int q = 0; q < TX; ++q)
+      if (ix0 + q < W) *reinterpret_cast<float4*>(out + (int64_t)(ix0 + q) * C) = acc[q];
+  }
+}
+
 // depthwise conv weight gradient: block = 64 channel quads x 4 pixel lanes over
 // one chunk of output pixels; K*K quad accumulators per thread; the 4 pixel
 // lanes are combined through LDS and each (chunk, channel, tap) partial is
@@ -192,6 +250,87 @@ __global__ __launch_bounds__(256) void dwconv_dw_partial(const float* __restrict
       dst[(int64_t)(c + 1) * KK + k] = s.y;
       dst[(int64_t)(c + 2) * KK + k] = s.z;
       dst[(int64_t)(c + 3) * KK + k] = s.w;
+    }
+    __syncthreads();
+  }
+}
+
+// stride-1 weight gradient with a row sweep: a work item is TX consecutive
+// output columns of one row; per tap row it loads the TX+K-1 input quads once
+// and the TX dy quads, and updates all K*K tap accumulators.
+template <int K, int TX>
+__global__ __launch_bounds__(256) void dwconv_dw_partial_s1(const float* __restrict__ dy, const float* __restrict__ x,
+                                                            float* __restrict__ part, int N, int H, int W, int C,
+                                                            int pad_t, int pad_l, int OH, int OW,
+                                                            int64_t grp_per_chunk) {
+  constexpr int KK = K * K, SPAN = TX + K - 1;
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int C4 = C >> 2;
+  const int c4 = blockIdx.x * 64 + lane;
+  const bool cok = c4 < C4;
+  const int c = (cok ? c4 : 0) * 4;
+  const int OWT = (OW + TX - 1) / TX;
+  const int64_t ngrp = (int64_t)N * OH * OWT;
+  const int64_t g0 = (int64_t)blockIdx.y * grp_per_chunk;
+  const int64_t g1 = min(ngrp, g0 + grp_per_chunk);
+  float4 acc[KK];
+#pragma unroll
+  for (int k = 0; k < KK; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (cok) {
+    for (int64_t gi = g0 + ty; gi < g1; gi += 4) {
+      const int oxt = (int)(gi % OWT);
+      const int64_t t = gi / OWT;
+      const int oy = (int)(t % OH);
+      const int n = (int)(t / OH);
+      const int ox0 = oxt * TX;
+      float4 g[TX];
+#pragma unroll
+      for (int q = 0; q < TX; ++q) {
+        g[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ox0 + q < OW) g[q] = *reinterpret_cast<const float4*>(dy + (((int64_t)n * OH + oy) * OW + ox0 + q) * C + c);
+      }
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky) {
+        const int iy = oy - pad_t + ky;
+        if (iy < 0 || iy >= H) continue;
+        const float* row = x + (((int64_t)n * H + iy) * W) * C + c;
+#pragma unroll
+        for (int j = 0; j < SPAN; ++j) {
+          const int ix = ox0 - pad_l + j;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ix >= 0 && ix < W) v = *reinterpret_cast<const float4*>(row + (int64_t)ix * C);
+#pragma unroll
+          for (int q = 0; q < TX; ++q) {
+            const int kx = j - q;
+            if (kx >= 0 && kx < K) {
+              float4& a = acc[ky * K + kx];
+              a.x = fmaf(g[q].x, v.x, a.x);
+              a.y = fmaf(g[q].y, v.y, a.y);
+              a.z = fmaf(g[q].z, v.z, a.z);
+              a.w = fmaf(g[q].w, v.w, a.w);
+            }
+          }
+        }
+      }
+    }
+  }
+  float* dst = part + (int64_t)blockIdx.y * C * KK;
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+    red[ty][lane] = acc[k];
+    __syncthreads();
+    if (ty == 0 && cok) {
+      float4 sum = red[0][lane];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        const float4 v = red[q][lane];
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+      }
+      dst[(int64_t)(c + 0) * KK + k] = sum.x;
+      dst[(int64_t)(c + 1) * KK + k] = sum.y;
+      dst[(int64_t)(c + 2) * KK + k] = sum.z;
+      dst[(int64_t)(c + 3) * KK + k] = sum.w;
     }
     __syncthreads();
   }
@@ -409,10 +548,22 @@ static void launch_dw_bwd(const float* dy, const float* x, const float* w, float
   if (dx) {
     constexpr int TX = 4;
     const int64_t total = (int64_t)N * H * ((W + TX - 1) / TX) * (C / 4);
-    hipLaunchKernelGGL((dwconv_dx_kernel<K, S, TX>), dim3(grid_1d(total)), dim3(256), 0, st, dy, w, dx, N, H, W, C,
-                       pt, pl, OH, OW);
+    if (S == 1)
+      hipLaunchKernelGGL((dwconv_dx_s1_kernel<K, TX>), dim3(grid_1d(total)), dim3(256), 0, st, dy, w, dx, N, H, W, C,
+                         pt, pl, OH, OW);
+    else
+      hipLaunchKernelGGL((dwconv_dx_kernel<K, S, TX>), dim3(grid_1d(total)), dim3(256), 0, st, dy, w, dx, N, H, W,
+                         C, pt, pl, OH, OW);
   }
-  if (part) {
+  if (part && S == 1) {
+    constexpr int TXW = 4;
+    const int64_t npix = (int64_t)N * OH * OW;
+    const int ch = dw_chunks(C, npix);
+    const int64_t ngrp = (int64_t)N * OH * ((OW + TXW - 1) / TXW);
+    dim3 grid((unsigned)cdiv(C / 4, 64), (unsigned)ch);
+    hipLaunchKernelGGL((dwconv_dw_partial_s1<K, TXW>), grid, dim3(256), 0, st, dy, x, part, N, H, W, C, pt, pl, OH,
+                       OW, cdiv(ngrp, ch));
+  } else if (part) {
     const int64_t npix = (int64_t)N * OH * OW;
     const int ch = dw_chunks(C, npix);
     dim3 grid((unsigned)cdiv(C / 4, 64), (unsigned)ch);

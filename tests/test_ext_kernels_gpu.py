@@ -54,7 +54,8 @@ def tf_same_ref(x, w, stride, groups):
 
 
 @pytest.mark.parametrize("k,s,hw,c", [(3, 1, (9, 13), 24), (3, 2, (10, 12), 16), (5, 1, (7, 11), 8),
-                                      (5, 2, (12, 17), 40), (5, 2, (15, 20), 12), (3, 2, (1, 1), 4)])
+                                      (5, 2, (12, 17), 40), (5, 2, (15, 20), 12), (3, 2, (1, 1), 4),
+                                      (5, 1, (30, 41), 264), (3, 1, (2, 3), 8), (5, 1, (1, 1), 4)])
 def test_dwconv_same(mf, k, s, hw, c):
     x, w = rnd(2, c, *hw, seed=1), rnd(c, 1, k, k, seed=2, scale=0.5)
     xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
