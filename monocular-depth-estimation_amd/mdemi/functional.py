@@ -41,10 +41,12 @@ def _split_for(M, N, K):
     ways (each split still >= 256 rows of K); their slabs are combined by a column sum."""
     tiles = math.ceil(M / 128) * math.ceil(N / 128)
     ktiles = math.ceil(K / 16)
-    if tiles >= 512 or ktiles < 32:
+    # tools/gemm_split_study.py (profiles/r02_split_study.log): >= 384 output tiles already
+    # fill the chip (a split only adds slab traffic); each split keeps >= 512 rows of K
+    if tiles >= 384 or ktiles < 32:
         return 1
-    target, cap = (_target_blocks(), 64) if tiles >= 8 else (2 * _target_blocks(), 512)
-    split = min(max(1, target // tiles), ktiles // 16, cap)
+    target, cap = (_target_blocks(), 128) if tiles >= 8 else (2 * _target_blocks(), 512)
+    split = min(max(1, target // tiles), ktiles // 32, cap)
     return max(1, split)
 
 
