@@ -165,6 +165,14 @@ int mdemi_layernorm_bwd(const float* dy, const float* x, const float* mean,
                         const float* rstd, const float* gamma, float* dx,
                         float* dgamma, float* dbeta, int64_t rows, int32_t C,
                         int32_t accumulate_dx, void* workspace, void* stream);
+/* Backward of a LayerNorm whose input also feeds a residual (skip) path,
+ * x -> (LN(x), x) in swin_transformer.py:200-245 / newcrf_layers.py:204-257:
+ * dx = LN'(dy) + dadd with dadd the skip path's gradient (may alias dx), so
+ * the two gradient contributions are summed in the same sweep. */
+int mdemi_layernorm_bwd_add(const float* dy, const float* x, const float* mean,
+                            const float* rstd, const float* gamma, const float* dadd, float* dx,
+                            float* dgamma, float* dbeta, int64_t rows, int32_t C,
+                            void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* (Shifted-)window multi-head attention with relative position bias.       */

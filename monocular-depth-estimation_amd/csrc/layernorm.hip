@@ -68,9 +68,9 @@ __global__ __launch_bounds__(LN_THREADS) void ln_fwd_kernel(const float* __restr
 template <int CACHE>
 __global__ __launch_bounds__(LN_THREADS) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                           const float* __restrict__ g, float* __restrict__ dx,
+                                                           const float* __restrict__ g, float* dx,
                                                            float* __restrict__ partial, int64_t rows, int C,
-                                                           int accumulate) {
+                                                           const float* addsrc) {
   __shared__ float4 red[LN_THREADS / 64][128];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t wave = ((int64_t)blockIdx.x * LN_THREADS + threadIdx.x) >> 6;
@@ -117,8 +117,8 @@ __global__ __launch_bounds__(LN_THREADS) void ln_bwd_kernel(const float* __restr
         o.y = rs * (gd[q].y - m1 - xh[q].y * m2);
         o.z = rs * (gd[q].z - m1 - xh[q].z * m2);
         o.w = rs * (gd[q].w - m1 - xh[q].w * m2);
-        if (accumulate) {
-          const float4 p = dxr[c4];
+        if (addsrc) {  // dx = LN'(dy) + addsrc (addsrc may be dx itself)
+          const float4 p = reinterpret_cast<const float4*>(addsrc + r * C)[c4];
           o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
         }
         dxr[c4] = o;
@@ -208,19 +208,18 @@ extern "C" size_t mdemi_layernorm_bwd_workspace_size(int64_t rows, int32_t C) {
   return ln_part_bytes(rows, C) + align_up((size_t)2 * C * 4, 256) + colsum_ws_bytes(ln_bwd_blocks(rows, C), 2 * C);
 }
 
-extern "C" int mdemi_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
-                                   const float* gamma, float* dx, float* dgamma, float* dbeta, int64_t rows,
-                                   int32_t C, int32_t accumulate_dx, void* workspace, void* stream) {
+static int ln_bwd_launch(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
+                         const float* addsrc, float* dx, float* dgamma, float* dbeta, int64_t rows, int32_t C,
+                         void* workspace, hipStream_t st) {
   MDEMI_REQUIRE(dy && x && mean && rstd && gamma && dx && rows > 0 && C > 0, "layernorm_bwd: bad args");
   MDEMI_REQUIRE(C % 4 == 0, "layernorm_bwd: C %% 4 != 0 (C=%d)", C);
   const int cache = ln_cache(C);
   MDEMI_REQUIRE(cache > 0, "layernorm_bwd: C=%d too large", C);
   if (!workspace) { set_error("layernorm_bwd: workspace required"); return MDEMI_EWORKSPACE; }
-  hipStream_t st = (hipStream_t)stream;
   const int nb = ln_bwd_blocks(rows, C);
   float* partial = (float*)workspace;
   LN_DISPATCH(cache, ln_bwd_kernel, dim3(nb), dim3(LN_THREADS), 0, st, dy, x, mean, rstd, gamma, dx, partial, rows,
-              C, accumulate_dx);
+              C, addsrc);
   if (dgamma || dbeta) {
     float* sums = (float*)((char*)workspace + ln_part_bytes(rows, C));
     void* cws = (char*)sums + align_up((size_t)2 * C * 4, 256);
@@ -229,4 +228,18 @@ extern "C" int mdemi_layernorm_bwd(const float* dy, const float* x, const float*
     hipLaunchKernelGGL(ln_param_split, dim3((C + 255) / 256), dim3(256), 0, st, sums, dgamma, dbeta, C);
   }
   return check_launch("layernorm_bwd");
+}
+
+extern "C" int mdemi_layernorm_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
+                                   const float* gamma, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                                   int32_t C, int32_t accumulate_dx, void* workspace, void* stream) {
+  return ln_bwd_launch(dy, x, mean, rstd, gamma, accumulate_dx ? dx : nullptr, dx, dgamma, dbeta, rows, C, workspace,
+                       (hipStream_t)stream);
+}
+
+extern "C" int mdemi_layernorm_bwd_add(const float* dy, const float* x, const float* mean, const float* rstd,
+                                       const float* gamma, const float* dadd, float* dx, float* dgamma, float* dbeta,
+                                       int64_t rows, int32_t C, void* workspace, void* stream) {
+  MDEMI_REQUIRE(dadd, "layernorm_bwd_add: dadd required");
+  return ln_bwd_launch(dy, x, mean, rstd, gamma, dadd, dx, dgamma, dbeta, rows, C, workspace, (hipStream_t)stream);
 }

@@ -112,6 +112,7 @@ _SIGS = {
     "mdemi_layernorm_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
     "mdemi_layernorm_bwd_workspace_size": (sz, [i64, i32]),
     "mdemi_layernorm_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp, vp]),
+    "mdemi_layernorm_bwd_add": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp, vp]),
     "mdemi_winattn_fwd_workspace_size": (sz, [ctypes.POINTER(WinAttnDesc)]),
     "mdemi_winattn_fwd": (ctypes.c_int, [ctypes.POINTER(WinAttnDesc), vp]),
     "mdemi_winattn_bwd_workspace_size": (sz, [ctypes.POINTER(WinAttnDesc)]),

@@ -477,6 +477,56 @@ class _LayerNormFn(torch.autograd.Function):
         return dx, dg, db, None
 
 
+class _LayerNormSkipFn(torch.autograd.Function):
+    """x -> (LayerNorm(x), x): a LayerNorm whose input is also the block's residual.  The two
+    gradient contributions to x meet inside the LayerNorm backward sweep
+    (mdemi_layernorm_bwd_add) instead of an extra elementwise add of autograd."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        _require_cuda(x, weight, bias)
+        x = _c(x)
+        C = x.shape[-1]
+        rows = x.numel() // C
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        L.call("mdemi_layernorm_fwd", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
+               mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), L.stream())
+        ctx.save_for_backward(x, weight, mean, rstd)
+        skip = x.view_as(x)
+        return y, skip
+
+    @staticmethod
+    def backward(ctx, dy, dskip):
+        x, weight, mean, rstd = ctx.saved_tensors
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dx = torch.empty_like(x)
+        dg = torch.empty(C, device=x.device, dtype=torch.float32)
+        db = torch.empty(C, device=x.device, dtype=torch.float32)
+        lib = L.load()
+        ws = L.workspace(lib.mdemi_layernorm_bwd_workspace_size(rows, C), x.device)
+        if dy is None:
+            return dskip, None, None, None
+        dy = _c(dy)
+        if dskip is None:
+            L.check(lib.mdemi_layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                            weight.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), rows, C,
+                                            0, ws.data_ptr(), L.stream()), "layernorm_bwd")
+        else:
+            dskip = _c(dskip)
+            L.check(lib.mdemi_layernorm_bwd_add(dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                                weight.data_ptr(), dskip.data_ptr(), dx.data_ptr(), dg.data_ptr(),
+                                                db.data_ptr(), rows, C, ws.data_ptr(), L.stream()), "layernorm_bwd_add")
+        return dx, dg, db, None
+
+
+def layer_norm_skip(x, weight, bias, eps=1e-5):
+    """(LayerNorm(x), x) for a residual block; use the second output as the residual."""
+    return _LayerNormSkipFn.apply(x, weight, bias, eps)
+
+
 def layer_norm(x, weight, bias, eps=1e-5):
     return _LayerNormFn.apply(x, weight, bias, eps)
 

@@ -67,10 +67,11 @@ class CRFBlock(nn.Module):
         assert Lq == H * W, "input feature has wrong size"
         x2 = x.reshape(B * Lq, C)
         v2 = v.reshape(B * Lq, v.shape[-1])
-        xn = mf.layer_norm(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        xn, x2 = mf.layer_norm_skip(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         a = self.attn.attend(xn, v2, B, H, W, self.shift_size)
         x2 = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x2)
-        x2 = self.mlp(mf.layer_norm(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps), residual=x2)
+        xn, x2 = mf.layer_norm_skip(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        x2 = self.mlp(xn, residual=x2)
         return x2.view(B, Lq, self.v_dim)
 
 

@@ -101,16 +101,19 @@ class SwinTransformerBlock(nn.Module):
         H, W = self.H, self.W
         assert Lq == H * W, "input feature has wrong size"
         x2 = x.reshape(B * Lq, C)
-        xn = mf.layer_norm(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        # layer_norm_skip: (LN(x), x) -- the residual's gradient is summed inside the LN backward
+        xn, x2 = mf.layer_norm_skip(x2, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         a = self.attn.attend(xn, B, H, W, self.shift_size)
         p = self.drop_path_prob if self.training else 0.0
         if p == 0.0:
             x2 = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x2)
-            x2 = self.mlp(mf.layer_norm(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps), residual=x2)
+            xn, x2 = mf.layer_norm_skip(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+            x2 = self.mlp(xn, residual=x2)
         else:
             br = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias)
             x2 = mf.drop_path_add(x2.view(B, -1), br.view(B, -1), p, True).view(B * Lq, C)
-            br = self.mlp(mf.layer_norm(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps))
+            xn, x2 = mf.layer_norm_skip(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+            br = self.mlp(xn)
             x2 = mf.drop_path_add(x2.view(B, -1), br.view(B, -1), p, True).view(B * Lq, C)
         return x2.view(B, Lq, C)
 

@@ -360,6 +360,26 @@ def test_batch_norm_running_stats(mf, momentum):
     assert int(bn.num_batches_tracked) == 3
 
 
+@pytest.mark.parametrize("rows,C", [(300, 64), (1000, 192), (77, 1536)])
+def test_layer_norm_skip(mf, rows, C):
+    """(LN(x), x) residual pattern: z = x + LN(x) W^T; the skip gradient is summed inside the
+    LayerNorm backward (mdemi_layernorm_bwd_add) -- value and all gradients vs fp64."""
+    x, g, b = rnd(rows, C, seed=80, scale=2), rnd(C, seed=81) + 1, rnd(C, seed=82)
+    w = rnd(C, C, seed=83, scale=0.1)
+    dz = rnd(rows, C, seed=84)
+    xr, gr, br = [t.clone().requires_grad_() for t in (x, g, b)]
+    zr = xr + F.layer_norm(xr, (C,), gr, br, 1e-5) @ w.t()
+    zr.backward(dz)
+    xg, gg, bg = [t.float().to(DEV).requires_grad_() for t in (x, g, b)]
+    y, skip = mf.layer_norm_skip(xg, gg, bg, 1e-5)
+    zg = mf.linear(y, w.float().to(DEV), None, residual=skip)
+    zg.backward(dz.float().to(DEV))
+    close(zg, zr, rtol=1e-5)
+    close(xg.grad, xr.grad, rtol=1e-4)
+    close(gg.grad, gr.grad, rtol=1e-4)
+    close(bg.grad, br.grad, rtol=1e-4)
+
+
 def test_pixel_shuffle_avgpool_patch(mf):
     n, c, h, w = 2, 16, 5, 7
     x = rnd(n, c, h, w, seed=70)

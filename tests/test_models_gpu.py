@@ -362,7 +362,8 @@ def test_adabins_end_to_end_vs_oracle():
         p, _ = oab.unet_adaptive_bins(P, img.to(P["conv_out.0.weight"].dtype), 1e-3, 10.0)
         (p * dy.to(p.dtype)).sum().backward()
 
-    assert _check_param_grads(m, sd, loss_fn) == len(list(m.parameters()))
+    # gradients through the restated B5 encoder: same 1e-3 basis as test_efficientnet_b5_encoder_vs_oracle
+    assert _check_param_grads(m, sd, loss_fn, rel=1e-3) == len(list(m.parameters()))
 
 
 # ---------------------------------------------------------------------------
@@ -416,4 +417,5 @@ def test_depthformer_v8_end_to_end_vs_oracle():
         d, _, _ = odf.depthformer_v8_full(P, img.to(P["decoder.aux_embedding"].dtype), opt, 1e-3, 10.0)
         (d * dy.to(d.dtype)).sum().backward()
 
-    assert _check_param_grads(m, sd, loss_fn) > 0
+    # gradients through the restated B5 encoder: same 1e-3 basis as test_efficientnet_b5_encoder_vs_oracle
+    assert _check_param_grads(m, sd, loss_fn, rel=1e-3) > 0
