@@ -166,10 +166,8 @@ def profiled_traffic(regex, workload):
             prof = json.load(f)
     except (OSError, ValueError):
         return None
-    ent = prof.get(workload, {})
-    if ent.get("kernel_regex") != regex:
-        return None
-    return ent.get("traffic_bytes_per_launch")
+    fam = prof.get(workload, {}).get("families", {}).get(regex)
+    return None if fam is None else fam.get("traffic_bytes_per_launch")
 
 
 def cpu_baseline(model, name, H, W, budget_s):
