@@ -142,6 +142,14 @@ int mdemi_depth_metrics(const float* pred, const float* gt, int32_t B, int32_t H
                         int32_t y1, int32_t x0, int32_t x1, float min_depth, float max_depth, int32_t clamp_pred,
                         double* out, void* workspace, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* Flip-eval (config eval.flip_eval): rows of W floats (an NCHW batch is     */
+/* B*C*H rows).  flip_w: y[r][w] = x[r][W-1-w] (out of place).              */
+/* flip_avg_w: y[r][w] = (a[r][w] + b[r][W-1-w]) / 2; y may alias a.        */
+/* ------------------------------------------------------------------------ */
+int mdemi_flip_w(const float* x, float* y, int64_t rows, int32_t W, void* stream);
+int mdemi_flip_avg_w(const float* a, const float* b, float* y, int64_t rows, int32_t W, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -167,6 +167,8 @@ _SIGS = {
     "mdemi_pad_fold_replicate": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
     "mdemi_depth_metrics_workspace_size": (sz, [i32, i32, i32]),
     "mdemi_depth_metrics": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, f32, i32, vp, vp, vp]),
+    "mdemi_flip_w": (ctypes.c_int, [vp, vp, i64, i32, vp]),
+    "mdemi_flip_avg_w": (ctypes.c_int, [vp, vp, vp, i64, i32, vp]),
 }
 
 _lib = None

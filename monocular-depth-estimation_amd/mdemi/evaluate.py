@@ -1,0 +1,70 @@
+"""Evaluation path on the GPU: inference, flip-eval, the
+9 depth metrics and their cross-rank mean.
+
+The reference's driver (run.py) is absent from the snapshot; what it did is
+fixed by the config keys eval.{min_depth_eval, max_depth_eval, garg_crop,
+eigen_crop, flip_eval} (json/{nyu,kitti}/*.json) and by the helpers it
+called: cal_eval_mask + tcompute_errors (utils/depth_utils.py:4-54),
+RunningAverageDict (utils/common_utils.py:92-135) and
+all_reduce_dict(op="mean") (utils/dist_utils.py:67-76).  Restated here (parity
+of the driver itself is unpinned; each helper is pinned by its own tests):
+
+  pred = model(img)                       # depth, NCHW
+  if flip_eval: pred = (pred + flip_w(model(flip_w(img)))) / 2
+  pred -> GT resolution (bilinear, align_corners=True) when the model
+          predicts at half resolution (AdaBins / Depthformer v8)
+  per image: metrics over crop & min_depth_eval < gt < max_depth_eval,
+             pred clamped into [min_depth_eval, max_depth_eval]
+
+Every step is a libmdemi launch (flip: mdemi_flip_w / mdemi_flip_avg_w;
+resize: mdemi_bilinear_*; metrics: mdemi_depth_metrics); only the per-image
+metric rows (B x 10 fp64) come back to the host.
+"""
+import torch
+
+from . import functional as mf
+from .utils.common_utils import RunningAverageDict
+from .utils.depth_utils import tcompute_errors_gpu
+from .utils.dist_utils import all_reduce_dict
+
+__all__ = ["predict_depth", "evaluate_batch", "evaluate"]
+
+
+def _depth_of(out):
+    # NewCRFDepth -> depth; UnetAdaptiveBins -> (pred, bin_edges); DepthformerV8 -> (depth, centers, attn)
+    return out[0] if isinstance(out, (tuple, list)) else out
+
+
+def predict_depth(model, img, flip_eval=False, size=None):
+    """Depth (B,1,H,W) for an NCHW image batch; flip-eval averages in the flipped pass; `size`
+    resizes the prediction (bilinear, align_corners=True) to the ground-truth resolution."""
+    with torch.no_grad():
+        pred = _depth_of(model(img))
+        if flip_eval:
+            pred = mf.flip_avg_w(pred, _depth_of(model(mf.flip_w(img))))
+        if size is not None and tuple(pred.shape[-2:]) != tuple(size):
+            B, _, h, w = pred.shape
+            pred = mf.interpolate_bilinear(pred.reshape(B, h, w, 1), size=tuple(size),
+                                           align_corners=True).reshape(B, 1, *size)
+    return pred
+
+
+def evaluate_batch(model, img, gt, eval_opt, data_type):
+    """Per-image metric dicts (the reference's keys) for one batch."""
+    pred = predict_depth(model, img, bool(eval_opt.get("flip_eval", False)), size=tuple(gt.shape[-2:]))
+    return tcompute_errors_gpu(pred, gt, eval_opt, data_type)
+
+
+def evaluate(model, batches, eval_opt, data_type):
+    """Running mean of the metrics over (img, gt) batches on this rank, then the mean over ranks
+    (all_reduce_dict op="mean"; a pass-through without a process group)."""
+    was_training = model.training
+    model.eval()
+    avg = RunningAverageDict()
+    try:
+        for img, gt in batches:
+            for m in evaluate_batch(model, img, gt, eval_opt, data_type):
+                avg.update(m)
+    finally:
+        model.train(was_training)
+    return all_reduce_dict(avg.get_value(), op="mean")

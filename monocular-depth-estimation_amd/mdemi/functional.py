@@ -1373,6 +1373,31 @@ def depth_metrics(pred, gt, rect, min_depth, max_depth, clamp_pred=True):
     return out
 
 
+def flip_w(x):
+    """x flipped along its last (width) dim, e.g. an NCHW image batch for flip-eval."""
+    _require_cuda(x)
+    x = _c(x)
+    y = torch.empty_like(x)
+    if x.numel():
+        w = x.shape[-1]
+        L.call("mdemi_flip_w", x.data_ptr(), y.data_ptr(), x.numel() // w, w, L.stream())
+    return y
+
+
+def flip_avg_w(a, b):
+    """(a + b flipped along width) / 2: the flip-eval average of a prediction and the
+    prediction of the flipped input."""
+    _require_cuda(a, b)
+    if a.shape != b.shape:
+        raise ValueError(f"flip_avg_w: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+    a, b = _c(a), _c(b)
+    y = torch.empty_like(a)
+    if a.numel():
+        w = a.shape[-1]
+        L.call("mdemi_flip_avg_w", a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel() // w, w, L.stream())
+    return y
+
+
 class _AttentionFn(torch.autograd.Function):
     """Multi-head scaled dot-product attention over column slices of token-major buffers
     ([B*S, ld] rows): per head h, P = softmax(scale * Q_h K_h^T) (returned, [B, heads, Sq, Sk]),

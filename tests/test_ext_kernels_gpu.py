@@ -325,3 +325,20 @@ def test_patch_conv_dgrad(mf):
     close(nchw(xg.grad), xr.grad, rtol=1e-4)
     close(wg.grad, wr.grad, rtol=1e-4)
     close(bg.grad, br.grad, rtol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 5, 16), (1, 1, 7, 13), (3, 2, 4, 1), (2, 3, 480, 640)])
+def test_flip_w_and_flip_avg(mf, shape):
+    """Flip-eval sweeps (eval.flip_eval): bit-exact flip, (a + flip(b)) / 2 in fp32; both the
+    float4 path (W % 4 == 0) and the scalar path, and an unaligned view."""
+    a, b = rnd(*shape, seed=60).float(), rnd(*shape, seed=61).float()
+    ag, bg = a.to(DEV), b.to(DEV)
+    assert torch.equal(mf.flip_w(ag).cpu(), torch.flip(a, dims=[-1]))
+    want = (a + torch.flip(b, dims=[-1])) * 0.5
+    assert torch.equal(mf.flip_avg_w(ag, bg).cpu(), want)
+    # storage offset of one float: the kernel must take the scalar path
+    buf = torch.zeros(a.numel() + 1, device=DEV)
+    buf[1:] = ag.reshape(-1)
+    av = buf[1:].view(shape)
+    assert torch.equal(mf.flip_w(av).cpu(), torch.flip(a, dims=[-1]))
+    assert torch.equal(mf.flip_avg_w(av, bg).cpu(), want)

@@ -419,3 +419,48 @@ def test_depthformer_v8_end_to_end_vs_oracle():
 
     # gradients through the restated B5 encoder: same 1e-3 basis as test_efficientnet_b5_encoder_vs_oracle
     assert _check_param_grads(m, sd, loss_fn, rel=1e-3) > 0
+
+
+def test_flip_eval_metrics_newcrfs_tiny07():
+    """GPU evaluation path (mdemi.evaluate): model -> flip-eval -> 9 metrics -> running mean,
+    against the fp64 oracle forward on the image and its mirror, averaged, and the reference's
+    metric formulas (oracle.metrics.compute_errors) over the NYU eigen crop."""
+    import numpy as np
+
+    from mdemi.evaluate import evaluate
+    from mdemi.model.NewCRFs import NewCRFDepth
+    from oracle import metrics as omet
+    from oracle import newcrfs as onc
+    from oracle.weights import closed_form_fill, rng_array
+
+    m = NewCRFDepth(version="tiny07", max_depth=10.0, drop_path_rate=0.0)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    closed_form_fill(sd, seed=0.3, scale=0.02)
+    m.load_state_dict(sd)
+    m = m.to(DEV)
+    H, W = 96, 128
+    img = torch.from_numpy(rng_array((2, 3, H, W), 21))
+    g = torch.Generator().manual_seed(5)
+    gt = torch.rand(2, 1, H, W, generator=g, dtype=torch.float64) * 9.0 + 0.5
+    gt[:, :, :10] = 0.0  # invalid rows
+    sd64 = {k: v.double() if torch.is_floating_point(v) else v for k, v in sd.items()}
+    ref = onc.newcrf_depth(sd64, img.double(), "tiny07", max_depth=10.0)
+    ref_f = onc.newcrf_depth(sd64, torch.flip(img.double(), dims=[-1]), "tiny07", max_depth=10.0)
+    ref = 0.5 * (ref + torch.flip(ref_f, dims=[-1]))
+    eval_opt = {"min_depth_eval": 1e-3, "max_depth_eval": 10.0, "garg_crop": False, "eigen_crop": True,
+                "flip_eval": True}
+    # NYU eigen crop at 96x128 is the full-frame rectangle (45:471, 41:601) -- use KITTI's relative one
+    got = evaluate(m, [(img.float().to(DEV), gt.float().to(DEV))], eval_opt, "KITTI")
+    mask = omet.cal_eval_mask(eval_opt, gt[0, 0].numpy(), "KITTI")
+    want = {}
+    for i in range(2):
+        p = np.clip(ref[i, 0].numpy(), 1e-3, 10.0)
+        gi = gt[i, 0].numpy()
+        valid = mask & (gi > 1e-3) & (gi < 10.0)
+        e = omet.compute_errors(gi[valid], p[valid])
+        for k, v in e.items():
+            want[k] = want.get(k, 0.0) + float(v) / 2
+    for k in ("a1", "a2", "a3", "abs_rel", "sq_rel", "rmse", "rmse_log", "silog", "log_10"):
+        # depth within 1e-4 rel (north_star); metrics follow; threshold metrics may flip one pixel
+        tol = 2.0 / mask.sum() if k in ("a1", "a2", "a3") else 1e-4 * abs(want[k]) + 1e-7
+        assert abs(got[k] - want[k]) <= tol, (k, got[k], want[k])
