@@ -44,15 +44,16 @@ WORKLOADS = {
                           ref_cfg="json/kitti/newcrfs/newcrfs_github_eval.json"),
     # BASELINE.json configs[1]: AdaBins (EfficientNet-B5 + DecoderBN + mViT + bin head), NYU bs=16;
     # json/nyu/adabins/adabins_cham_per_batch.json: AdamW lr 3.57e-4 wd 0.1, grad_norm 0.1, SILog a10 b0.15
-    # (its chamfer bin loss, weight 0.1, is not built)
+    # + its chamfer bin loss (loss.chamfer_weight 0.1) on the bin edges
     "adabins": dict(model="AdaBins-B5", h=480, w=640, batch=16, max_depth=10.0, lr=3.57e-4, wd=0.1, beta=0.15,
-                    per_image=False, workload="AdaBins EfficientNet-B5 train step, NYU 480x640",
+                    per_image=False, chamfer=0.1, workload="AdaBins EfficientNet-B5 train step, NYU 480x640",
                     ref_cfg="json/nyu/adabins/adabins_cham_per_batch.json"),
     # Depthformer v8 (json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json model/optimizer
-    # block: hidden 256, 4 heads, 256 bins / aux tokens, lr 3.2e-4 wd 0.1, SILog a10 b0.5 per image) at the
+    # block: hidden 256, 4 heads, 256 bins / aux tokens, lr 3.2e-4 wd 0.1, SILog a10 b0.5 per image,
+    # chamfer 0.1 on the bin centres) at the
     # NYU crop, fp32 (BASELINE configs[4]'s bf16 + hipGraph variant is not built)
     "depthformer": dict(model="DepthformerV8-B5", h=480, w=640, batch=8, max_depth=10.0, lr=3.2e-4, wd=0.1,
-                        beta=0.5, per_image=True, workload="Depthformer v8 train step, NYU 480x640 (fp32)",
+                        beta=0.5, per_image=True, chamfer=0.1, workload="Depthformer v8 train step, NYU 480x640 (fp32)",
                         ref_cfg="json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json"),
 }
 DFV8_OPT = {"hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256, "img_size": [480, 640],
@@ -106,14 +107,29 @@ def build(args, device):
         model = NewCRFDepth(version="large07", inv_depth=False, max_depth=cfg["max_depth"])
     model = model.to(device).train()
     opt = FusedAdamW(model.parameters(), lr=cfg.get("lr", 2e-5), weight_decay=cfg.get("wd", 0.0), max_grad_norm=0.1)
-    loss_fn = SILogLoss(alpha=10.0, beta=cfg.get("beta", 0.15), per_image=cfg.get("per_image", False), min_depth=1e-3)
-    return model, opt, loss_fn
+    silog = SILogLoss(alpha=10.0, beta=cfg.get("beta", 0.15), per_image=cfg.get("per_image", False), min_depth=1e-3)
+    return model, opt, TrainLoss(silog, cfg.get("chamfer", 0.0), from_edges=(args.model == "adabins"))
+
+
+class TrainLoss:
+    """SILog on the depth (+ chamfer_weight x the bin chamfer loss on AdaBins' edges / Depthformer's
+    centres when the config sets loss.chamfer_weight)."""
+
+    def __init__(self, silog, chamfer_weight, from_edges):
+        from mdemi.train import BinsChamferLoss
+        self.silog, self.w = silog, float(chamfer_weight)
+        self.chamfer = BinsChamferLoss(1e-3, from_edges=from_edges) if self.w > 0 else None
+
+    def __call__(self, out, gt):
+        pred = out[0] if isinstance(out, tuple) else out  # AdaBins / Depthformer: (depth at H/2, bins, ...)
+        loss = self.silog(pred, gt)  # SILogLoss upsamples a half-resolution prediction to the GT first
+        if self.chamfer is not None:
+            loss = loss + self.w * self.chamfer(out[1], gt)
+        return loss
 
 
 def train_step(model, opt, loss_fn, img, gt, ddp=None):
-    out = model(img)
-    pred = out[0] if isinstance(out, tuple) else out  # AdaBins / Depthformer: (depth at H/2, ...)
-    loss = loss_fn(pred, gt)  # SILogLoss upsamples a half-resolution prediction to the GT first
+    loss = loss_fn(model(img), gt)
     loss.backward()
     if ddp is not None:
         ddp.finish()
@@ -184,20 +200,24 @@ def cpu_baseline(model, name, H, W, budget_s):
     img, gt = synthetic_batch(1, H, W, "cpu", seed=1)
     if name == "adabins":
         from oracle import adabins as oab
-        fwd = lambda: oab.unet_adaptive_bins(P, img, 1e-3, cfg["max_depth"])[0]  # noqa: E731
+        fwd = lambda: oab.unet_adaptive_bins(P, img, 1e-3, cfg["max_depth"])  # noqa: E731
     elif name == "depthformer":
         from oracle import depthformer as odf
         opt_m = dict(DFV8_OPT, attn_drop_prob=0.0, drop_prob=0.0)
-        fwd = lambda: odf.depthformer_v8_full(P, img, opt_m, 1e-3, cfg["max_depth"])[0]  # noqa: E731
+        fwd = lambda: odf.depthformer_v8_full(P, img, opt_m, 1e-3, cfg["max_depth"])  # noqa: E731
     else:
         from oracle import newcrfs as onc
         fwd = lambda: onc.newcrf_depth(P, img, "large07", max_depth=cfg["max_depth"])  # noqa: E731
 
     def step():
-        pred = fwd()
+        out = fwd()
+        pred = out[0] if isinstance(out, tuple) else out
         if pred.shape[-2:] != gt.shape[-2:]:
             pred = torch.nn.functional.interpolate(pred, gt.shape[-2:], mode="bilinear", align_corners=True)
         loss = omet.silog_loss(pred, gt, 1e-3, 10.0, cfg.get("beta", 0.15), cfg.get("per_image", False))
+        if cfg.get("chamfer", 0.0) > 0:
+            from oracle.adabins import bins_chamfer_loss
+            loss = loss + cfg["chamfer"] * bins_chamfer_loss(out[1], gt, 1e-3, from_edges=(name == "adabins"))
         loss.backward()
         torch.nn.utils.clip_grad_norm_(params, 0.1)
         opt.step()
@@ -212,7 +232,7 @@ def cpu_baseline(model, name, H, W, budget_s):
         step()
     dt = (time.perf_counter() - t0) / n
     return {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle {cfg['model']} fp32 train step (fwd+SILog+bwd+AdamW), batch 1 at {H}x{W}, "
+            "sample": f"oracle {cfg['model']} fp32 train step (fwd+SILog{'+chamfer' if cfg.get('chamfer') else ''}+bwd+AdamW), batch 1 at {H}x{W}, "
                       f"{n} timed steps after 1 warm-up, {threads} threads, {os.cpu_count()} host CPUs visible"}
 
 

@@ -150,6 +150,21 @@ int mdemi_depth_metrics(const float* pred, const float* gt, int32_t B, int32_t H
 int mdemi_flip_w(const float* x, float* y, int64_t rows, int32_t W, void* stream);
 int mdemi_flip_avg_w(const float* a, const float* b, float* y, int64_t rows, int32_t W, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* AdaBins bin-centre chamfer loss (cfg loss.chamfer_weight; upstream        */
+/* BinsChamferLoss over pytorch3d chamfer_distance -- the reference's loss  */
+/* module is absent, parity unpinned).  from_edges: edges [B][P+1] (AdaBins) */
+/* else centres [B][P] (Depthformer v8); gt [B][HW]; targets              */
+/* are gt >= thresh.  fwd writes the batch-mean loss (loss[0]) and          */
+/* dloss/dcentres [B][P] (gcent); bwd: dedges = dloss[0] (device scalar) *   */
+/* the centre gradients pushed onto both edges of each bin.                 */
+/* ------------------------------------------------------------------------ */
+size_t mdemi_bins_chamfer_workspace_size(int32_t B, int32_t P, int64_t HW);
+int mdemi_bins_chamfer_fwd(const float* edges, const float* gt, int32_t B, int32_t P, int32_t from_edges, int64_t HW,
+                           float thresh, float* loss, float* gcent, void* workspace, void* stream);
+int mdemi_bins_chamfer_bwd(const float* gcent, const float* dloss, float* dedges, int32_t B, int32_t P,
+                           int32_t from_edges, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,234 @@
+// AdaBins bin-centre chamfer loss (config loss.chamfer_weight, e.g.
+// json/nyu/adabins/adabins_cham_per_batch.json).  The reference snapshot's
+// loss module is absent; restated from upstream AdaBins' BinsChamferLoss over
+// pytorch3d.chamfer_distance defaults (squared distance, point mean, batch
+// mean) -- parity unpinned, see oracle/adabins.py:bins_chamfer_loss.
+//
+// Per image b, x = the P bin centres c_i = (e_i + e_{i+1}) / 2 (AdaBins passes the
+// edges) or the centres themselves (Depthformer v8's output), y = the valid
+// ground-truth depths (gt >= thresh), N_y of them:
+//   cham_x = (1/P)   sum_i min_t (c_i - t)^2
+//   cham_y = (1/N_y) sum_t min_i (c_i - t)^2
+//   loss   = (1/B) sum_b (cham_x + cham_y)
+// and, with t*(i) the nearest target of centre i and S_i / n_i the sum / count
+// of the targets whose nearest centre is i (first index on ties, as argmin):
+//   dloss/dc_i = (1/B) [ (2/P)(c_i - t*(i)) + (2/N_y)(n_i c_i - S_i) ]
+//
+// One workgroup per (1024-pixel chunk, image): the centres and the chunk sit in
+// LDS; pass 1 gives each pixel its nearest centre, pass 2 gives each centre
+// its nearest pixel and the (n_i, S_i) of the chunk -- both are broadcast LDS
+// reads, and every partial is combined in a fixed order (deterministic).  The
+// GT map is read once: 4 B per pixel from HBM; the P x HW distance work is
+// VALU (2 * P flops per pixel per pass).
+#include <math.h>
+
+#include "common.h"
+#include "mdemi_ext.h"
+
+namespace mdemi {
+
+constexpr int CH_PIX = 1024;  // pixels per workgroup
+constexpr int CH_NT = 256;
+
+__global__ void __launch_bounds__(CH_NT) chamfer_partial(const float* __restrict__ edges, const float* __restrict__ gt,
+                                                         int32_t P, int32_t fe, int64_t HW, float thresh, int32_t nchunk,
+                                                         float* __restrict__ pmin, float* __restrict__ pt,
+                                                         float* __restrict__ pcnt, float* __restrict__ psum,
+                                                         double* __restrict__ pdy, double* __restrict__ pn) {
+  extern __shared__ float lds[];
+  float* cen = lds;                // [P]
+  float* val = cen + P;            // [CH_PIX]
+  int* nn = (int*)(val + CH_PIX);  // [CH_PIX] nearest centre, -1 = invalid
+  __shared__ double red[CH_NT / 64][2];
+  const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const float* e = edges + (int64_t)b * (P + fe);
+  for (int i = tid; i < P; i += CH_NT) cen[i] = fe ? 0.5f * (e[i] + e[i + 1]) : e[i];
+  const int64_t base = (int64_t)chunk * CH_PIX;
+  const float* g = gt + (int64_t)b * HW;
+  for (int k = tid; k < CH_PIX; k += CH_NT) {
+    const int64_t idx = base + k;
+    const float v = idx < HW ? g[idx] : 0.f;
+    val[k] = v;
+    nn[k] = (idx < HW && v >= thresh) ? 0 : -1;
+  }
+  __syncthreads();
+  // pass 1: nearest centre of each valid pixel
+  double dy = 0.0, ny = 0.0;
+  for (int k = tid; k < CH_PIX; k += CH_NT) {
+    if (nn[k] < 0) continue;
+    const float v = val[k];
+    float best = INFINITY;
+    int bi = 0;
+    for (int i = 0; i < P; ++i) {
+      const float d = (cen[i] - v) * (cen[i] - v);
+      if (d < best) { best = d; bi = i; }
+    }
+    nn[k] = bi;
+    dy += (double)best;
+    ny += 1.0;
+  }
+  // fixed-order block sums of (dy, ny)
+  for (int o = 32; o > 0; o >>= 1) {
+    dy += __shfl_xor(dy, o, 64);
+    ny += __shfl_xor(ny, o, 64);
+  }
+  if ((tid & 63) == 0) { red[tid >> 6][0] = dy; red[tid >> 6][1] = ny; }
+  __syncthreads();
+  const int64_t slot = (int64_t)b * nchunk + chunk;
+  if (tid == 0) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int w = 0; w < CH_NT / 64; ++w) { s0 += red[w][0]; s1 += red[w][1]; }
+    pdy[slot] = s0;
+    pn[slot] = s1;
+  }
+  // pass 2: per centre, nearest valid pixel of the chunk and the chunk's (n_i, S_i)
+  for (int i = tid; i < P; i += CH_NT) {
+    const float c = cen[i];
+    float best = INFINITY, bt = 0.f, cnt = 0.f, sum = 0.f;
+    for (int k = 0; k < CH_PIX; ++k) {
+      const int j = nn[k];
+      if (j < 0) continue;
+      const float v = val[k];
+      const float d = (c - v) * (c - v);
+      if (d < best) { best = d; bt = v; }
+      if (j == i) { cnt += 1.f; sum += v; }
+    }
+    const int64_t o = slot * P + i;
+    pmin[o] = best;
+    pt[o] = bt;
+    pcnt[o] = cnt;
+    psum[o] = sum;
+  }
+}
+
+__global__ void __launch_bounds__(CH_NT) chamfer_final(const float* __restrict__ edges, int32_t B, int32_t P, int32_t fe,
+                                                       int32_t nchunk, const float* __restrict__ pmin,
+                                                       const float* __restrict__ pt, const float* __restrict__ pcnt,
+                                                       const float* __restrict__ psum, const double* __restrict__ pdy,
+                                                       const double* __restrict__ pn, double* __restrict__ lossb,
+                                                       float* __restrict__ gcent) {
+  __shared__ double red[CH_NT / 64][3];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  double dy = 0.0, ny = 0.0;
+  for (int c = tid; c < nchunk; c += CH_NT) {
+    dy += pdy[(int64_t)b * nchunk + c];
+    ny += pn[(int64_t)b * nchunk + c];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    dy += __shfl_xor(dy, o, 64);
+    ny += __shfl_xor(ny, o, 64);
+  }
+  if ((tid & 63) == 0) { red[tid >> 6][0] = dy; red[tid >> 6][1] = ny; }
+  __syncthreads();
+  double DY = 0.0, NY = 0.0;
+  for (int w = 0; w < CH_NT / 64; ++w) { DY += red[w][0]; NY += red[w][1]; }
+  __syncthreads();
+  const float* e = edges + (int64_t)b * (P + fe);
+  const double invB = 1.0 / B;
+  double cx = 0.0;
+  for (int i = tid; i < P; i += CH_NT) {
+    float best = INFINITY, bt = 0.f;
+    double cnt = 0.0, sum = 0.0;
+    for (int c = 0; c < nchunk; ++c) {
+      const int64_t o = ((int64_t)b * nchunk + c) * P + i;
+      const float m = pmin[o];
+      if (m < best) { best = m; bt = pt[o]; }
+      cnt += pcnt[o];
+      sum += psum[o];
+    }
+    const double ci = fe ? (double)(0.5f * (e[i] + e[i + 1])) : (double)e[i];
+    double g = 0.0;
+    if (NY > 0.0) {
+      cx += (double)best;
+      g = (2.0 / P) * (ci - (double)bt) + (2.0 / NY) * (cnt * ci - sum);
+    }
+    gcent[(int64_t)b * P + i] = (float)(invB * g);
+  }
+  for (int o = 32; o > 0; o >>= 1) cx += __shfl_xor(cx, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6][2] = cx;
+  __syncthreads();
+  if (tid == 0) {
+    double CX = 0.0;
+    for (int w = 0; w < CH_NT / 64; ++w) CX += red[w][2];
+    lossb[b] = NY > 0.0 ? CX / P + DY / NY : 0.0;
+  }
+}
+
+__global__ void chamfer_mean(const double* __restrict__ lossb, int32_t B, float* __restrict__ loss) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double s = 0.0;
+    for (int b = 0; b < B; ++b) s += lossb[b];
+    loss[0] = (float)(s / B);
+  }
+}
+
+// edges: dedges[b][k] = dloss * (gcent[b][k-1] + gcent[b][k]) / 2 (centres k-1 and k share edge k);
+// centres given directly (fe == 0): dcentres = dloss * gcent
+__global__ void chamfer_bwd_kernel(const float* __restrict__ gcent, const float* __restrict__ dloss,
+                                   float* __restrict__ dedges, int32_t B, int32_t P, int32_t fe) {
+  const int64_t n = (int64_t)B * (P + fe);
+  const float dl = dloss[0];
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = t / (P + fe);
+    const int k = (int)(t - b * (P + fe));
+    const float* g = gcent + b * P;
+    if (!fe) {
+      dedges[t] = dl * g[k];
+      continue;
+    }
+    float s = 0.f;
+    if (k >= 1) s += g[k - 1];
+    if (k < P) s += g[k];
+    dedges[t] = dl * 0.5f * s;
+  }
+}
+
+static int chamfer_chunks(int64_t HW) { return (int)((HW + CH_PIX - 1) / CH_PIX); }
+
+}  // namespace mdemi
+
+using namespace mdemi;
+
+extern "C" size_t mdemi_bins_chamfer_workspace_size(int32_t B, int32_t P, int64_t HW) {
+  const size_t nc = (size_t)chamfer_chunks(HW);
+  return align_up((size_t)B * nc * P * 4 * sizeof(float), 256) + align_up((size_t)B * nc * 2 * sizeof(double), 256) +
+         align_up((size_t)B * sizeof(double), 256);
+}
+
+extern "C" int mdemi_bins_chamfer_fwd(const float* edges, const float* gt, int32_t B, int32_t P, int32_t from_edges,
+                                      int64_t HW, float thresh, float* loss, float* gcent, void* workspace,
+                                      void* stream) {
+  MDEMI_REQUIRE(edges && gt && loss && gcent && B > 0 && P > 0 && P <= 4096 && HW > 0, "bins_chamfer_fwd: bad args");
+  if (!workspace) { set_error("bins_chamfer_fwd: workspace required"); return MDEMI_EWORKSPACE; }
+  const int32_t fe = from_edges ? 1 : 0;
+  const int nc = chamfer_chunks(HW);
+  const size_t np = (size_t)B * nc * P;
+  char* w = (char*)workspace;
+  float* pmin = (float*)w;
+  float* pt = pmin + np;
+  float* pcnt = pt + np;
+  float* psum = pcnt + np;
+  w += align_up(np * 4 * sizeof(float), 256);
+  double* pdy = (double*)w;
+  double* pn = pdy + (size_t)B * nc;
+  w += align_up((size_t)B * nc * 2 * sizeof(double), 256);
+  double* lossb = (double*)w;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)(P + CH_PIX) * sizeof(float) + CH_PIX * sizeof(int);
+  hipLaunchKernelGGL(chamfer_partial, dim3(nc, B), dim3(CH_NT), lds, st, edges, gt, P, fe, HW, thresh, nc, pmin, pt, pcnt,
+                     psum, pdy, pn);
+  hipLaunchKernelGGL(chamfer_final, dim3(B), dim3(CH_NT), 0, st, edges, B, P, fe, nc, pmin, pt, pcnt, psum, pdy, pn, lossb,
+                     gcent);
+  hipLaunchKernelGGL(chamfer_mean, dim3(1), dim3(64), 0, st, lossb, B, loss);
+  return check_launch("bins_chamfer_fwd");
+}
+
+extern "C" int mdemi_bins_chamfer_bwd(const float* gcent, const float* dloss, float* dedges, int32_t B, int32_t P,
+                                      int32_t from_edges, void* stream) {
+  MDEMI_REQUIRE(gcent && dloss && dedges && B > 0 && P > 0, "bins_chamfer_bwd: bad args");
+  const int32_t fe = from_edges ? 1 : 0;
+  const int64_t n = (int64_t)B * (P + fe);
+  const unsigned grid = (unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024);
+  hipLaunchKernelGGL(chamfer_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, gcent, dloss, dedges, B, P, fe);
+  return check_launch("bins_chamfer_bwd");
+}

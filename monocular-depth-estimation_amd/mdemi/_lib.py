@@ -169,6 +169,9 @@ _SIGS = {
     "mdemi_depth_metrics": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, f32, f32, i32, vp, vp, vp]),
     "mdemi_flip_w": (ctypes.c_int, [vp, vp, i64, i32, vp]),
     "mdemi_flip_avg_w": (ctypes.c_int, [vp, vp, vp, i64, i32, vp]),
+    "mdemi_bins_chamfer_workspace_size": (sz, [i32, i32, i64]),
+    "mdemi_bins_chamfer_fwd": (ctypes.c_int, [vp, vp, i32, i32, i32, i64, f32, vp, vp, vp, vp]),
+    "mdemi_bins_chamfer_bwd": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp]),
 }
 
 _lib = None

@@ -1,4 +1,6 @@
-"""SILog loss (restated; config keys loss.alpha / loss.beta / loss.per_image).
+"""SILog loss (restated; config keys loss.alpha / loss.beta / loss.per_image) and
+the AdaBins bin chamfer loss (config key loss.chamfer_weight; restated from
+upstream AdaBins' BinsChamferLoss -- the reference's loss module is absent).
 AdaBins / Depthformer predictions are at half resolution and are resized to
 the ground truth with bilinear align_corners=True first (upstream AdaBins
 convention; parity unpinned)."""
@@ -20,3 +22,19 @@ class SILogLoss(nn.Module):
             pred = mf.interpolate_bilinear(pred.reshape(B, h, w, 1), size=tuple(gt.shape[-2:]),
                                            align_corners=True).reshape(B, 1, *gt.shape[-2:])
         return mf.silog_loss(pred, gt, self.min_depth, self.alpha, self.beta, self.per_image, self.unbiased)
+
+
+class BinsChamferLoss(nn.Module):
+    """Chamfer distance between each image's bin centres and its valid (>= 1e-3) GT depths:
+    mean over centres of the squared distance to the nearest depth plus mean over depths of
+    the squared distance to the nearest centre, averaged over the batch (one libmdemi sweep
+    forward, one backward)."""
+
+    def __init__(self, thresh=1e-3, from_edges=True):
+        super().__init__()
+        self.thresh, self.from_edges = float(thresh), bool(from_edges)
+
+    def forward(self, bins, gt):
+        """bins: edges (B, P+1) (AdaBins), or centres (B, P, 1, 1) with from_edges=False
+        (Depthformer v8)."""
+        return mf.bins_chamfer(bins, gt, self.thresh, self.from_edges)

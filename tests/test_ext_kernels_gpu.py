@@ -342,3 +342,47 @@ def test_flip_w_and_flip_avg(mf, shape):
     av = buf[1:].view(shape)
     assert torch.equal(mf.flip_w(av).cpu(), torch.flip(a, dims=[-1]))
     assert torch.equal(mf.flip_avg_w(av, bg).cpu(), want)
+
+
+@pytest.mark.parametrize("B,P,H,W", [(2, 16, 9, 13), (3, 256, 40, 70), (1, 7, 1, 1500)])
+def test_bins_chamfer_loss_fwd_bwd(mf, B, P, H, W):
+    """AdaBins chamfer loss (loss.chamfer_weight) vs the fp64 oracle restatement, loss and edge
+    gradients; invalid (< 1e-3) GT pixels, several 1024-pixel chunks, ragged last chunk."""
+    from oracle.adabins import bins_chamfer_loss
+    g = torch.Generator().manual_seed(70 + P)
+    widths = torch.rand(B, P, generator=g, dtype=torch.float64) + 0.1
+    edges = torch.cat([torch.zeros(B, 1, dtype=torch.float64), widths.cumsum(1)], 1)
+    edges = 1e-3 + edges / edges[:, -1:] * (10.0 - 1e-3)
+    gt = torch.rand(B, 1, H, W, generator=g, dtype=torch.float64) * 9.5 + 0.5
+    gt[torch.rand(B, 1, H, W, generator=g) < 0.3] = 0.0
+    er = edges.clone().requires_grad_()
+    ref = bins_chamfer_loss(er, gt)
+    ref.backward()
+    eg = edges.float().to(DEV).requires_grad_()
+    got = mf.bins_chamfer(eg, gt.float().to(DEV))
+    got.backward(torch.tensor(1.7, device=DEV))
+    close(got, ref.detach(), rtol=1e-5, atol=1e-7)
+    close(eg.grad, 1.7 * er.grad, rtol=1e-4, atol=1e-7)
+
+
+def test_bins_chamfer_loss_from_centres(mf):
+    """Depthformer v8 form: centres (B, P, 1, 1) given directly (the oracle's chamfer, restated on
+    centres)."""
+    g = torch.Generator().manual_seed(77)
+    B, P = 2, 32
+    cen = torch.sort(torch.rand(B, P, generator=g, dtype=torch.float64) * 10, dim=1).values
+    gt = torch.rand(B, 1, 30, 50, generator=g, dtype=torch.float64) * 9.5 + 0.5
+    gt[:, :, :5] = 0.0
+    cr = cen.clone().requires_grad_()
+    d_ref = 0.0
+    for c, t in zip(cr, gt.flatten(1)):
+        t = t[t >= 1e-3]
+        d = (c[:, None] - t[None, :]) ** 2
+        d_ref = d_ref + d.min(1).values.mean() + d.min(0).values.mean()
+    d_ref = d_ref / B
+    d_ref.backward()
+    cg = cen.float().to(DEV).view(B, P, 1, 1).requires_grad_()
+    got = mf.bins_chamfer(cg, gt.float().to(DEV), from_edges=False)
+    got.backward()
+    close(got, d_ref.detach(), rtol=1e-5, atol=1e-7)
+    close(cg.grad.view(B, P), cr.grad, rtol=1e-4, atol=1e-7)
