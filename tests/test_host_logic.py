@@ -1,0 +1,42 @@
+"""CPU checks of host-side pieces added around the hot path: the oracle's
+bin chamfer restatement on a hand-worked case (the loss module is absent from
+the reference, so this pins the restatement to its published definition) and
+the RunningAverage(Dict) mirror (utils/common_utils.py:92-135)."""
+import torch
+
+from mdemi.utils.common_utils import RunningAverage, RunningAverageDict
+from oracle.adabins import bins_chamfer_loss
+
+
+def test_chamfer_oracle_hand_worked():
+    # edges 0,1,2,3 -> centres .5 1.5 2.5; targets .5, 2.4 (0.0 is below 1e-3: dropped)
+    e = torch.tensor([[0.0, 1.0, 2.0, 3.0]], dtype=torch.float64, requires_grad=True)
+    gt = torch.tensor([[[[0.5, 2.4, 0.0]]]], dtype=torch.float64)
+    loss = bins_chamfer_loss(e, gt)
+    # cham_x = (0 + 0.81 + 0.01) / 3 ; cham_y = (0 + 0.01) / 2
+    assert abs(loss.item() - ((0.81 + 0.01) / 3 + 0.01 / 2)) < 1e-12
+    loss.backward()
+    # dL/dc = (2/3)(c - t*) + (2/2) sum_{t -> c}(c - t): c0: 0, c1: (2/3)(-0.9), c2: (2/3)(0.1) + (0.1)
+    gc = torch.tensor([0.0, -0.6, 2 / 3 * 0.1 + 0.1], dtype=torch.float64)
+    want = torch.zeros(4, dtype=torch.float64)
+    want[:3] += 0.5 * gc
+    want[1:] += 0.5 * gc
+    assert torch.allclose(e.grad[0], want, atol=1e-12)
+    # the centres form gives the same loss
+    c = 0.5 * (e.detach()[:, 1:] + e.detach()[:, :-1])
+    assert abs(bins_chamfer_loss(c.view(1, 3, 1, 1), gt, from_edges=False).item() - loss.item()) < 1e-12
+
+
+def test_running_average_dict():
+    r = RunningAverage()
+    for v in (1.0, torch.tensor(2.0), 6.0):
+        r.append(v)
+    assert r.count == 3 and abs(r.avg - 3.0) < 1e-12
+    d = RunningAverageDict()
+    d.reset()  # no-op before the first update, as in the reference
+    d.update({"a1": 0.5, "rmse": 2.0})
+    d.update({"a1": 1.0, "rmse": 4.0})
+    assert d.get_value() == {"a1": 0.75, "rmse": 3.0}
+    d.reset()
+    d.update({"a1": 0.25, "rmse": 1.0})
+    assert d.get_value() == {"a1": 0.25, "rmse": 1.0}
