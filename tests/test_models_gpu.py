@@ -464,3 +464,43 @@ def test_flip_eval_metrics_newcrfs_tiny07():
         # depth within 1e-4 rel (north_star); metrics follow; threshold metrics may flip one pixel
         tol = 2.0 / mask.sum() if k in ("a1", "a2", "a3") else 1e-4 * abs(want[k]) + 1e-7
         assert abs(got[k] - want[k]) <= tol, (k, got[k], want[k])
+
+
+@pytest.mark.parametrize("H,W,max_depth,data_type", [(480, 640, 10.0, "NYU"), (352, 1216, 80.0, "KITTI")])
+def test_large07_full_size_depth_and_abs_rel_parity(H, W, max_depth, data_type):
+    """north_star's parity bar at the benchmark configurations: NeW-CRFs Swin-L (large07) forward
+    on one full NYU 480x640 / KITTI 352x1216 crop through libmdemi vs the fp64 oracle restatement
+    (pinned to the reference by the golden fixtures): depth within 1e-4 relative, and abs_rel /
+    RMSE over the eigen crop equal to 4 significant figures."""
+    import numpy as np
+
+    from mdemi.model.NewCRFs import NewCRFDepth
+    from mdemi.utils.depth_utils import tcompute_errors_gpu
+    from oracle import metrics as omet
+    from oracle import newcrfs as onc
+    from oracle.weights import closed_form_fill, rng_array
+
+    torch.set_num_threads(16)
+    m = NewCRFDepth(version="large07", max_depth=max_depth, drop_path_rate=0.0)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    closed_form_fill(sd, seed=0.11, scale=0.02)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()  # training-mode BatchNorm, as the oracle
+    img = torch.from_numpy(rng_array((1, 3, H, W), 31))
+    with torch.no_grad():
+        depth = m(img.float().to(DEV)).double().cpu()
+        ref = onc.newcrf_depth({k: v.double() if torch.is_floating_point(v) else v for k, v in sd.items()},
+                               img.double(), "large07", max_depth=max_depth)
+    err = (depth - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 1e-4 * scale, f"depth max|err| {err:.3e} vs max {scale:.3e}"
+    g = torch.Generator().manual_seed(9)
+    gt = ref * (0.8 + 0.4 * torch.rand(ref.shape, generator=g, dtype=torch.float64))
+    eo = {"min_depth_eval": 1e-3, "max_depth_eval": max_depth, "garg_crop": False, "eigen_crop": True}
+    got = tcompute_errors_gpu(depth.float().to(DEV), gt.float().to(DEV), eo, data_type)[0]
+    mask = omet.cal_eval_mask(eo, gt[0, 0].numpy(), data_type)
+    gi, pi = gt[0, 0].numpy(), np.clip(ref[0, 0].numpy(), 1e-3, max_depth)
+    valid = mask & (gi > 1e-3) & (gi < max_depth)
+    want = omet.compute_errors(gi[valid], pi[valid])
+    for k in ("abs_rel", "rmse"):
+        assert float(f"{got[k]:.4g}") == float(f"{want[k]:.4g}"), (k, got[k], want[k])
