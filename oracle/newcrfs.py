@@ -217,23 +217,28 @@ def newcrf(P, pre, x, v, heads, ws=7, depth=2):  # newcrf_layers.py:418-433 (+ B
 # ---------------------------------------------------------------------------
 # PSP head (uper_crf_head.py) with mmcv ConvModule semantics
 # ---------------------------------------------------------------------------
-def conv_module(P, pre, x, padding=0):
-    """mmcv ConvModule: conv (bias only without norm) -> BN/GN (training stats) -> ReLU."""
+def conv_module(P, pre, x, padding=0, bn_eval=False):
+    """mmcv ConvModule: conv (bias only without norm) -> BN/GN -> ReLU.  BN uses the batch
+    statistics (training) or, with bn_eval, the running statistics (model.eval())."""
     x = F.conv2d(x, P[pre + "conv.weight"], P.get(pre + "conv.bias"), padding=padding)
     if pre + "bn.weight" in P:
-        x = F.batch_norm(x, None, None, P[pre + "bn.weight"], P[pre + "bn.bias"], training=True, eps=1e-5)
+        if bn_eval:
+            x = F.batch_norm(x, P[pre + "bn.running_mean"], P[pre + "bn.running_var"], P[pre + "bn.weight"],
+                             P[pre + "bn.bias"], training=False, eps=1e-5)
+        else:
+            x = F.batch_norm(x, None, None, P[pre + "bn.weight"], P[pre + "bn.bias"], training=True, eps=1e-5)
     elif pre + "gn.weight" in P:
         x = F.group_norm(x, 256, P[pre + "gn.weight"], P[pre + "gn.bias"], eps=1e-5)
     return F.relu(x)
 
 
-def psp(P, pre, feats, pool_scales=(1, 2, 3, 6)):  # uper_crf_head.py:350-364 + PPM :46-58
+def psp(P, pre, feats, pool_scales=(1, 2, 3, 6), bn_eval=False):  # uper_crf_head.py:350-364 + PPM :46-58
     x = feats[-1]
     outs = [x]
     for i, s in enumerate(pool_scales):
         y = conv_module(P, f"{pre}psp_modules.{i}.1.", F.adaptive_avg_pool2d(x, s))
         outs.append(F.interpolate(y, size=x.shape[2:], mode="bilinear", align_corners=False))
-    return conv_module(P, pre + "bottleneck.", torch.cat(outs, 1), padding=1)
+    return conv_module(P, pre + "bottleneck.", torch.cat(outs, 1), padding=1, bn_eval=bn_eval)
 
 
 def disp_head(P, pre, x, scale):  # NewCRFDepth.py:151-164,185-188
@@ -250,11 +255,11 @@ VERSIONS = {  # NewCRFDepth.py:27-41
 }
 
 
-def newcrf_depth(P, imgs, version="large07", max_depth=100.0):  # NewCRFDepth.py:123-148
+def newcrf_depth(P, imgs, version="large07", max_depth=100.0, bn_eval=False):  # NewCRFDepth.py:123-148
     cfg = VERSIONS[version[:-2]]
     ws = int(version[-2:])
     feats = swin_transformer(P, "backbone.", imgs, cfg["depths"], cfg["num_heads"], ws)
-    ppm_out = psp(P, "decoder.", feats)
+    ppm_out = psp(P, "decoder.", feats, bn_eval=bn_eval)
     e3 = F.pixel_shuffle(newcrf(P, "crf3.", feats[3], ppm_out, 32), 2)
     e2 = F.pixel_shuffle(newcrf(P, "crf2.", feats[2], e3, 16), 2)
     e1 = F.pixel_shuffle(newcrf(P, "crf1.", feats[1], e2, 8), 2)

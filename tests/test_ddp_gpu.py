@@ -7,7 +7,7 @@ NeW-CRFs train step.  The mean of the per-rank gradients must equal the
 per-shard gradients averaged on one replica, and every rank must end with the
 same gradients.  RCCL itself only differs in the transport."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -19,12 +19,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 H, W = 64, 96
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+def _rendezvous():
+    """A fresh file:// rendezvous (no TCP port to race for)."""
+    fd, path = tempfile.mkstemp(prefix="mdemi_gloo_gpu_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _model_and_shard(rank):
@@ -40,14 +40,12 @@ def _model_and_shard(rank):
     return m, img, gt
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, path, q):
     import sys
     for p in (ROOT, os.path.join(ROOT, "monocular-depth-estimation_amd")):
         sys.path.insert(0, p)
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         from mdemi.train import GradAllReduce, SILogLoss, broadcast_parameters
         m, img, gt = _model_and_shard(rank)
@@ -71,8 +69,8 @@ def test_grad_allreduce_gpu_gradients_two_ranks():
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    path = _rendezvous()
+    procs = [ctx.Process(target=_worker, args=(r, world, path, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:

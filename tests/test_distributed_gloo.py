@@ -3,7 +3,7 @@ utils.dist_utils mirror (dist_utils.py:15-89 semantics) and GradAllReduce's
 bucketing / hook-driven launch / mean, with the GPU pack/unpack sweeps
 swapped for torch ops (the only difference from the RCCL path)."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -11,26 +11,24 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+def _rendezvous():
+    """A fresh file:// rendezvous (no TCP port to race for between picking and binding)."""
+    fd, path = tempfile.mkstemp(prefix="mdemi_gloo_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
-def _init(rank, world, port):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _init(rank, world, path):
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
 
 
-def _dist_utils_worker(rank, world, port, q):
+def _dist_utils_worker(rank, world, path, q):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "monocular-depth-estimation_amd"))
     try:
-        _init(rank, world, port)
+        _init(rank, world, path)
         from mdemi.utils import dist_utils as du
         res = {}
         res["sum"] = du.all_reduce_scalar(rank + 1.0, "sum")
@@ -76,12 +74,12 @@ class _CPUGradAllReduce:
         return G(model, bucket_mb=bucket_mb)
 
 
-def _ddp_worker(rank, world, port, q):
+def _ddp_worker(rank, world, path, q):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "monocular-depth-estimation_amd"))
     try:
-        _init(rank, world, port)
+        _init(rank, world, path)
         from mdemi.train.ddp import broadcast_parameters
         torch.manual_seed(100 + rank)  # different init per rank: broadcast must fix it
         model = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64),
@@ -104,8 +102,8 @@ def _ddp_worker(rank, world, port, q):
 def _spawn(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    path = _rendezvous()
+    procs = [ctx.Process(target=fn, args=(r, world, path, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=120) for _ in range(world))

@@ -444,8 +444,9 @@ def test_flip_eval_metrics_newcrfs_tiny07():
     gt = torch.rand(2, 1, H, W, generator=g, dtype=torch.float64) * 9.0 + 0.5
     gt[:, :, :10] = 0.0  # invalid rows
     sd64 = {k: v.double() if torch.is_floating_point(v) else v for k, v in sd.items()}
-    ref = onc.newcrf_depth(sd64, img.double(), "tiny07", max_depth=10.0)
-    ref_f = onc.newcrf_depth(sd64, torch.flip(img.double(), dims=[-1]), "tiny07", max_depth=10.0)
+    # evaluate() runs model.eval(): BatchNorm on running statistics in the oracle too
+    ref = onc.newcrf_depth(sd64, img.double(), "tiny07", max_depth=10.0, bn_eval=True)
+    ref_f = onc.newcrf_depth(sd64, torch.flip(img.double(), dims=[-1]), "tiny07", max_depth=10.0, bn_eval=True)
     ref = 0.5 * (ref + torch.flip(ref_f, dims=[-1]))
     eval_opt = {"min_depth_eval": 1e-3, "max_depth_eval": 10.0, "garg_crop": False, "eigen_crop": True,
                 "flip_eval": True}
