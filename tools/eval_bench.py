@@ -1,0 +1,60 @@
+"""Throughput of the GPU evaluation path: NeW-CRFs-L07 inference with flip-eval,
+resize-free metrics over the eigen crop, RunningAverageDict -- images/sec on synthetic NYU/KITTI
+batches (random-init weights, model.eval()).
+
+  python tools/eval_bench.py [--model newcrfs|newcrfs_kitti] [--batch 8] [--steps 10] [--no-flip]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "monocular-depth-estimation_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="newcrfs", choices=["newcrfs", "newcrfs_kitti"])
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-flip", action="store_true")
+    a = ap.parse_args()
+    import bench
+    from mdemi.evaluate import evaluate_batch
+    from mdemi.model.NewCRFs import NewCRFDepth
+    from mdemi.utils.common_utils import RunningAverageDict
+
+    cfg = bench.WORKLOADS[a.model]
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = NewCRFDepth(version="large07", max_depth=cfg["max_depth"]).to(dev).eval()
+    img, gt = bench.synthetic_batch(a.batch, cfg["h"], cfg["w"], dev, seed=5)
+    dtype = "KITTI" if a.model == "newcrfs_kitti" else "NYU"
+    eo = {"min_depth_eval": 1e-3, "max_depth_eval": cfg["max_depth"], "garg_crop": False, "eigen_crop": True,
+          "flip_eval": not a.no_flip}
+    avg = RunningAverageDict()
+    for _ in range(a.warmup):
+        for m in evaluate_batch(model, img, gt, eo, dtype):
+            avg.update(m)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        for m in evaluate_batch(model, img, gt, eo, dtype):  # per-image rows come back to the host
+            avg.update(m)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"metric": f"images/sec (eval, flip_eval={not a.no_flip}) {cfg['model']} {cfg['w']}x{cfg['h']}",
+                      "value": round(a.batch * a.steps / dt, 3), "unit": "images/sec", "batch": a.batch,
+                      "steps": a.steps, "ms_per_batch": round(dt / a.steps * 1e3, 2), "dtype": "fp32",
+                      "abs_rel": avg.get_value()["abs_rel"]}))
+
+
+if __name__ == "__main__":
+    main()
