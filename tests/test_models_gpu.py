@@ -505,3 +505,25 @@ def test_large07_full_size_depth_and_abs_rel_parity(H, W, max_depth, data_type):
     want = omet.compute_errors(gi[valid], pi[valid])
     for k in ("abs_rel", "rmse"):
         assert float(f"{got[k]:.4g}") == float(f"{want[k]:.4g}"), (k, got[k], want[k])
+
+
+def test_graphed_predictor_matches_eager():
+    """hipGraph-captured inference (flip-eval) replays bit-identically to the eager path, for two
+    different inputs through the same capture."""
+    from mdemi.evaluate import GraphedPredictor, predict_depth
+    from mdemi.model.NewCRFs import NewCRFDepth
+    from oracle.weights import closed_form_fill, rng_array
+
+    m = NewCRFDepth(version="tiny07", max_depth=10.0, drop_path_rate=0.0)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    closed_form_fill(sd, seed=0.5, scale=0.02)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    a = torch.from_numpy(rng_array((2, 3, 64, 96), 3)).float().to(DEV)
+    b = torch.from_numpy(rng_array((2, 3, 64, 96), 4)).float().to(DEV)
+    gp = GraphedPredictor(m, a, flip_eval=True)
+    for x in (a, b, a):
+        got = gp(x)
+        want = predict_depth(m, x, flip_eval=True)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want)

@@ -25,9 +25,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-flip", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay the inference as one captured hipGraph")
     a = ap.parse_args()
     import bench
-    from mdemi.evaluate import evaluate_batch
+    from mdemi.evaluate import GraphedPredictor, evaluate_batch
     from mdemi.model.NewCRFs import NewCRFDepth
     from mdemi.utils.common_utils import RunningAverageDict
 
@@ -40,6 +41,8 @@ def main():
     eo = {"min_depth_eval": 1e-3, "max_depth_eval": cfg["max_depth"], "garg_crop": False, "eigen_crop": True,
           "flip_eval": not a.no_flip}
     avg = RunningAverageDict()
+    if a.graph:
+        model = GraphedPredictor(model, img, flip_eval=eo["flip_eval"])
     for _ in range(a.warmup):
         for m in evaluate_batch(model, img, gt, eo, dtype):
             avg.update(m)
@@ -50,7 +53,8 @@ def main():
             avg.update(m)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(json.dumps({"metric": f"images/sec (eval, flip_eval={not a.no_flip}) {cfg['model']} {cfg['w']}x{cfg['h']}",
+    print(json.dumps({"metric": f"images/sec (eval, flip_eval={not a.no_flip}, graph={a.graph}) "
+                                f"{cfg['model']} {cfg['w']}x{cfg['h']}",
                       "value": round(a.batch * a.steps / dt, 3), "unit": "images/sec", "batch": a.batch,
                       "steps": a.steps, "ms_per_batch": round(dt / a.steps * 1e3, 2), "dtype": "fp32",
                       "abs_rel": avg.get_value()["abs_rel"]}))
