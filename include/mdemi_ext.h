@@ -165,6 +165,19 @@ int mdemi_bins_chamfer_fwd(const float* edges, const float* gt, int32_t B, int32
 int mdemi_bins_chamfer_bwd(const float* gcent, const float* dloss, float* dedges, int32_t B, int32_t P,
                            int32_t from_edges, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* Conv weight re-layouts (reference [Cout][Cin][KH][KW] <-> GEMM operands): */
+/* OHWI: out[co][ky][kx][c] = w[co][c][ky][kx]  (fwd, patch-conv dgrad)     */
+/* OIHW: out[co][c][ky][kx] = w[co][ky][kx][c]  (wgrad -> parameter layout) */
+/* DGRAD: out[ky][kx][co][c] = w[co][c][KH-1-ky][KW-1-kx] (input gradient)   */
+/* Out of place; cout/cin/kh/kw always describe the conv.                   */
+/* ------------------------------------------------------------------------ */
+#define MDEMI_WL_OHWI 0
+#define MDEMI_WL_OIHW 1
+#define MDEMI_WL_DGRAD 2
+int mdemi_conv_weight_layout(const float* w, float* out, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
+                             int32_t mode, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

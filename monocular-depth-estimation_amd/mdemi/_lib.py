@@ -37,6 +37,7 @@ ACT_NONE, ACT_GELU, ACT_RELU, ACT_LEAKY, ACT_GELU_GRAD, ACT_SIGMOID = 0, 1, 2, 3
 ACT_SILU, ACT_RELU_GRAD, ACT_SILU_GRAD = 6, 7, 8
 ACT_GRAD_OF = {ACT_GELU: ACT_GELU_GRAD, ACT_RELU: ACT_RELU_GRAD, ACT_SILU: ACT_SILU_GRAD}
 BINS_RELU, BINS_ELU = 0, 1  # include/mdemi_ext.h
+WL_OHWI, WL_OIHW, WL_DGRAD = 0, 1, 2  # include/mdemi_ext.h (mdemi_conv_weight_layout)
 PAD_ZERO, PAD_REPLICATE = 0, 1
 EW_ADD, EW_SIGMOID_SCALE, EW_SIGMOID_SCALE_BWD, EW_AXPBY, EW_ACT_BWD = 0, 1, 2, 3, 4
 
@@ -172,6 +173,7 @@ _SIGS = {
     "mdemi_bins_chamfer_workspace_size": (sz, [i32, i32, i64]),
     "mdemi_bins_chamfer_fwd": (ctypes.c_int, [vp, vp, i32, i32, i32, i64, f32, vp, vp, vp, vp]),
     "mdemi_bins_chamfer_bwd": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp]),
+    "mdemi_conv_weight_layout": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
 }
 
 _lib = None

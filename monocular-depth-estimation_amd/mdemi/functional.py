@@ -276,7 +276,7 @@ class _Conv2dFn(torch.autograd.Function):
             oh, ow = out_hw
         M, K = n * oh * ow, kh * kw * c
         out = torch.empty(n, oh, ow, cout, device=x.device, dtype=torch.float32)
-        wf = weight.permute(0, 2, 3, 1).reshape(cout, K).contiguous()
+        wf = conv_weight_layout(weight, L.WL_OHWI).view(cout, K)
         pointwise = kh == 1 and kw == 1 and stride == 1 and pad == 0
         if pointwise:
             gemm(x, wf, out, M, cout, K, lda=c, ldb=K, ldc=cout, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
@@ -317,7 +317,7 @@ class _Conv2dFn(torch.autograd.Function):
             elif stride == kh == kw and pad == 0 and not ctx.explicit:
                 # non-overlapping patches (mViT embedding_encoder): column gradients by one GEMM
                 # against the (ky,kx,c)-ordered weight, then a scatter back to the NHWC pixels
-                wf = weight.permute(0, 2, 3, 1).reshape(cout, K).contiguous()
+                wf = conv_weight_layout(weight, L.WL_OHWI).view(cout, K)
                 dcols = torch.empty(M, K, device=dy.device, dtype=torch.float32)
                 gemm(dy, wf, dcols, M, K, cout, lda=cout, ldb=K, ldc=K, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
                 dx = torch.empty_like(x)
@@ -327,7 +327,7 @@ class _Conv2dFn(torch.autograd.Function):
                 if stride != 1 or ctx.explicit:
                     raise NotImplementedError("conv2d dgrad: stride 1 or stride == kernel only")
                 # dX = conv(dY, flip(W)^T) with pad k-1-p:  Wd[(ky,kx,co)][c] = W[co][c][k-1-ky][k-1-kx]
-                wd = weight.flip(2, 3).permute(2, 3, 0, 1).reshape(kh * kw * cout, cin).contiguous()
+                wd = conv_weight_layout(weight, L.WL_DGRAD).view(kh * kw * cout, cin)
                 dx = torch.empty_like(x)
                 if pad_mode == L.PAD_ZERO:
                     gemm(dy, wd, dx, n * h * w, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
@@ -353,7 +353,7 @@ class _Conv2dFn(torch.autograd.Function):
             else:
                 gemm(dy, x, dwf, cout, K, M, lda=cout, ldb=0, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_CONV,
                      conv=_geom(n, h, w, c, oh, ow, kh, kw, stride, pad, pad_mode), rowsum_a=db)
-            dw = dwf.view(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()
+            dw = conv_weight_layout(dwf, L.WL_OIHW, (cout, cin, kh, kw))
         elif want_db:
             colsum(dy.reshape(-1, cout), out=db)
         return dx, dw, db, None, None, None, None, None
@@ -1370,6 +1370,21 @@ def depth_metrics(pred, gt, rect, min_depth, max_depth, clamp_pred=True):
     L.check(lib.mdemi_depth_metrics(pred.data_ptr(), gt.data_ptr(), b, h, w, y0, y1, x0, x1, float(min_depth),
                                     float(max_depth), int(clamp_pred), out.data_ptr(), ws.data_ptr(), L.stream()),
             "depth_metrics")
+    return out
+
+
+def conv_weight_layout(w, mode, conv_shape=None):
+    """Conv weight re-layout on the GPU (mdemi_conv_weight_layout): L.WL_OHWI / L.WL_DGRAD take
+    the reference's [Cout][Cin][KH][KW] weight; L.WL_OIHW takes [Cout][KH][KW][Cin] data and
+    returns the parameter layout (conv_shape = (Cout, Cin, KH, KW) names the conv).  1x1
+    OHWI/OIHW re-layouts are identities and return a view."""
+    cout, cin, kh, kw = conv_shape if conv_shape is not None else w.shape
+    w = _c(w)
+    if kh == 1 and kw == 1 and mode != L.WL_DGRAD:
+        return w.view(cout, cin, 1, 1) if mode == L.WL_OIHW else w.view(cout, 1, 1, cin)
+    shape = {L.WL_OHWI: (cout, kh, kw, cin), L.WL_OIHW: (cout, cin, kh, kw), L.WL_DGRAD: (kh, kw, cout, cin)}[mode]
+    out = torch.empty(shape, device=w.device, dtype=torch.float32)
+    L.call("mdemi_conv_weight_layout", w.data_ptr(), out.data_ptr(), cout, cin, kh, kw, mode, L.stream())
     return out
 
 

@@ -534,3 +534,18 @@ def test_gemm_variants_bit_identical(mf, layouts):
         close(c, ref, rtol=1e-5 * math.sqrt(K))
         same = [o for o in outs if o[1] == split][0][2]
         assert torch.equal(c, same), f"variant {v} split {split} differs bitwise"
+
+
+@pytest.mark.parametrize("cout,cin,kh,kw", [(8, 12, 3, 3), (5, 7, 5, 5), (16, 3, 4, 4), (6, 10, 1, 1), (4, 4, 1, 3)])
+def test_conv_weight_layout(cout, cin, kh, kw):
+    """mdemi_conv_weight_layout against the torch permutations it replaces (bit-exact)."""
+    from mdemi import _lib as L
+    from mdemi import functional as mf
+    g = torch.Generator().manual_seed(cout * 100 + cin)
+    w = torch.randn(cout, cin, kh, kw, generator=g)
+    wg = w.to("cuda")
+    assert torch.equal(mf.conv_weight_layout(wg, L.WL_OHWI).cpu(), w.permute(0, 2, 3, 1))
+    assert torch.equal(mf.conv_weight_layout(wg, L.WL_DGRAD).cpu(), w.flip(2, 3).permute(2, 3, 0, 1))
+    ohwi = w.permute(0, 2, 3, 1).contiguous()
+    got = mf.conv_weight_layout(ohwi.to("cuda"), L.WL_OIHW, (cout, cin, kh, kw)).cpu()
+    assert torch.equal(got, w)
