@@ -36,15 +36,15 @@ def main():
         if n is None or n in seen:
             continue
         seen.add(n)
-        for nxt, _ in n.next_functions:
+        for nxt, slot in n.next_functions:
             if nxt is not None:
-                uses[nxt] += 1
+                uses[(nxt, slot)] += 1  # per output slot: two outputs of one node are not summed
                 stack.append(nxt)
     fan = collections.Counter()
-    for n, u in uses.items():
+    for (n, _), u in uses.items():
         if u > 1 and type(n).__name__ != "AccumulateGrad":
             fan[type(n).__name__] += u - 1
-    acc = sum(u - 1 for n, u in uses.items() if u > 1 and type(n).__name__ == "AccumulateGrad")
+    acc = sum(u - 1 for (n, _), u in uses.items() if u > 1 and type(n).__name__ == "AccumulateGrad")
     print(f"backward nodes {len(seen)}; extra consumers (=> accumulation adds) by producer node type:")
     for k, v in fan.most_common():
         print(f"  {v:4d}  {k}")
