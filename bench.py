@@ -3,24 +3,30 @@
 
 metric (BASELINE.json): images/sec (train step) NYU 640x480 bs=8/GPU.
 Default workload: NeW-CRFs Swin-L (large07) train step at NYU 480x640, batch 8
-per GPU — the reference config json/nyu/newcrfs/newcrfs_github_eval.json
-(batch_size 8, loss alpha 10 / beta 0.15, AdamW lr 2e-5 wd 0, grad_norm 0.1).
-A step = forward + SILog loss + backward + clip + AdamW update (+ the RCCL
-gradient all-reduce when N > 1), all on libmdemi kernels; synthetic inputs
-(SURVEY §8d): ImageNet-normalised uniform images, NYU-style depth U(0.5, 10)
-inside the [45:472, 43:608] valid region.
+per GPU, built from the reference config json/nyu/newcrfs/newcrfs_github_eval.json
+by mdemi.train.build_from_config (the restated run.py construction): SILog
+alpha 10 / beta 0.15, AdamW lr 2e-5 wd 0 with OneCycle, grad_norm 0.1.
+A step = forward + loss + backward + (N > 1: bucketed RCCL gradient all-reduce
+overlapped with the backward) + clipped AdamW update + scheduler step, all on
+libmdemi kernels; synthetic inputs.  The same line carries a
+secondary measurement at the north_star shape (NeW-CRFs KITTI 352x1216, bs 8/GPU;
+BASELINE configs[2], and configs[3] when N = 8).
 
-  python bench.py [--gpus N --steps K --warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
+  python bench.py [--gpus N --steps K --warmup W]        (N > 1: starts N ranks itself)
+  torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+  python bench.py --config json/kitti/adabins/adabins_cham_per_batch_4gpu.json
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
 from __future__ import annotations
 
 import argparse
+import copy
 import json
-import math
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,35 +39,57 @@ import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (v_mfma_f32_32x32x2_f32)
 HBM_PEAK_GBS = 8000.0
+CPU_SHARE_PER_GPU = 16  # the GPU box's host-CPU share per GPU (OMP_NUM_THREADS there)
+
+# The reference configs that define each workload (the keys build_from_config reads; the
+# reference tree is not on the GPU box, so they are restated here with their source).
+_NEWCRFS_NYU = {  # json/nyu/newcrfs/newcrfs_github_eval.json
+    "model": {"name": "newcrfs"}, "loss": {"alpha": 10.0, "beta": 0.15, "per_image": False},
+    "dataset": {"data_type": "NYU"}, "dataloader": {"batch_size": 8},
+    "optimizer": {"lr": 2e-5, "weight_decay": 0.0},
+    "scheduler": {"name": "onecycle", "pct_start": 0.3, "div_factor": 25, "final_div_factor": 100},
+    "train": {"epoch": 25, "num_accum": 1, "grad_norm": 0.1},
+    "eval": {"max_depth_eval": 10, "min_depth_eval": 0.001, "garg_crop": False, "eigen_crop": True}}
+_NEWCRFS_KITTI = copy.deepcopy(_NEWCRFS_NYU)  # json/kitti/newcrfs/newcrfs_github_eval.json
+_NEWCRFS_KITTI["dataset"]["data_type"] = "KITTI"
+_NEWCRFS_KITTI["eval"].update(max_depth_eval=80, garg_crop=True, eigen_crop=False)
+_ADABINS_NYU = {  # json/nyu/adabins/adabins_cham_per_batch.json (batch 16: BASELINE configs[1])
+    "model": {"name": "adabins", "num_bins": 256, "bn_momentum": 0.1},
+    "loss": {"alpha": 10.0, "beta": 0.15, "per_image": False, "chamfer_weight": 0.1},
+    "dataset": {"data_type": "NYU"}, "dataloader": {"batch_size": 16},
+    "optimizer": {"lr": 0.000357, "weight_decay": 0.1},
+    "scheduler": {"name": "onecycle", "pct_start": 0.3, "div_factor": 25, "final_div_factor": 100},
+    "train": {"epoch": 25, "num_accum": 1, "grad_norm": 0.1},
+    "eval": {"max_depth_eval": 10, "min_depth_eval": 0.001, "garg_crop": False, "eigen_crop": True}}
+_DFV8_NYU = {  # json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json at the NYU crop
+    "model": {"name": "depthformer_v8", "hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256,
+              "img_size": [480, 640], "bn_momentum": 0.1, "attn_drop_prob": 0.1, "drop_prob": 0.2},
+    "loss": {"alpha": 10.0, "beta": 0.5, "per_image": True, "chamfer_weight": 0.1},
+    "dataset": {"data_type": "NYU"}, "dataloader": {"batch_size": 8},
+    "optimizer": {"lr": 0.00032, "weight_decay": 0.1},
+    "scheduler": {"name": "onecycle", "pct_start": 0.15, "div_factor": 25, "final_div_factor": 100},
+    "train": {"epoch": 50, "num_accum": 1, "grad_norm": 0.1},
+    "eval": {"max_depth_eval": 10, "min_depth_eval": 0.001, "garg_crop": False, "eigen_crop": True}}
 
 WORKLOADS = {
-    "newcrfs": dict(model="NewCRFs-L07", h=480, w=640, batch=8, max_depth=10.0,
+    "newcrfs": dict(opt=_NEWCRFS_NYU, model="NewCRFs-L07", h=480, w=640,
                     workload="NewCRFs Swin-L (large07) train step, NYU 480x640",
                     ref_cfg="json/nyu/newcrfs/newcrfs_github_eval.json"),
-    # BASELINE.json configs[2] / north_star target shape
-    "newcrfs_kitti": dict(model="NewCRFs-L07", h=352, w=1216, batch=8, max_depth=80.0,
+    "newcrfs_kitti": dict(opt=_NEWCRFS_KITTI, model="NewCRFs-L07", h=352, w=1216,
                           workload="NewCRFs Swin-L (large07) train step, KITTI 352x1216",
                           ref_cfg="json/kitti/newcrfs/newcrfs_github_eval.json"),
-    # BASELINE.json configs[1]: AdaBins (EfficientNet-B5 + DecoderBN + mViT + bin head), NYU bs=16;
-    # json/nyu/adabins/adabins_cham_per_batch.json: AdamW lr 3.57e-4 wd 0.1, grad_norm 0.1, SILog a10 b0.15
-    # + its chamfer bin loss (loss.chamfer_weight 0.1) on the bin edges
-    "adabins": dict(model="AdaBins-B5", h=480, w=640, batch=16, max_depth=10.0, lr=3.57e-4, wd=0.1, beta=0.15,
-                    per_image=False, chamfer=0.1, workload="AdaBins EfficientNet-B5 train step, NYU 480x640",
+    "adabins": dict(opt=_ADABINS_NYU, model="AdaBins-B5", h=480, w=640,
+                    workload="AdaBins EfficientNet-B5 train step, NYU 480x640",
                     ref_cfg="json/nyu/adabins/adabins_cham_per_batch.json"),
-    # Depthformer v8 (json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json model/optimizer
-    # block: hidden 256, 4 heads, 256 bins / aux tokens, lr 3.2e-4 wd 0.1, SILog a10 b0.5 per image,
-    # chamfer 0.1 on the bin centres) at the
-    # NYU crop, fp32 (BASELINE configs[4]'s bf16 + hipGraph variant is not built)
-    "depthformer": dict(model="DepthformerV8-B5", h=480, w=640, batch=8, max_depth=10.0, lr=3.2e-4, wd=0.1,
-                        beta=0.5, per_image=True, chamfer=0.1, workload="Depthformer v8 train step, NYU 480x640 (fp32)",
+    "depthformer": dict(opt=_DFV8_NYU, model="DepthformerV8-B5", h=480, w=640,
+                        workload="Depthformer v8 train step, NYU 480x640 (fp32)",
                         ref_cfg="json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json"),
 }
-DFV8_OPT = {"hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256, "img_size": [480, 640],
-            "attn_drop_prob": 0.1, "drop_prob": 0.2}
 # HBM bytes per launch of the roofline kernel family, from the committed
 # rocprofv3 --pmc passes (tools/pmc_traffic.py; FETCH_SIZE doubled per the
 # gfx950 correction).  None when no profile matches the kernel.
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+KERNEL_NAME = {0: "KCONTIG", 1: "MNCONTIG", 2: "CONV"}
 
 
 def parse():
@@ -70,77 +98,85 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="newcrfs", choices=sorted(WORKLOADS))
+    ap.add_argument("--config", default=None, help="a reference-format JSON config (overrides --model)")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the KITTI 352x1216 secondary line")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: launcher/gloo plumbing check only (a toy model, not a measurement)")
     return ap.parse_args()
 
 
-def synthetic_batch(B, H, W, device, seed):
+# --------------------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a torchrun environment: run N ranks (one per GPU) under
+    torch.distributed.run as a child process, before this process touches the GPU, and
+    return its exit code."""
+    if args.device == "cuda":
+        visible = torch.cuda.device_count()  # does not initialise the GPU on this image
+        if args.gpus > visible:
+            print(f"bench: --gpus {args.gpus} but only {visible} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+# --------------------------------------------------------------------------- data
+def synthetic_batch(B, H, W, device, seed, data_type="NYU"):
+    """ImageNet-normalised uniform images; NYU depth U(0.5, 10) inside the
+    [45:472, 43:608] valid region, KITTI depth U(1, 80) at a Bernoulli(0.15) LiDAR-like mask."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     img = torch.rand(B, 3, H, W, generator=g)
     mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
     std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
     img = (img - mean) / std  # depth_dataset.py:290 (ImageNet Normalize)
-    gt = torch.rand(B, 1, H, W, generator=g) * 9.5 + 0.5
-    valid = torch.zeros(B, 1, H, W)
-    valid[:, :, 45 * H // 480:472 * H // 480, 43 * W // 640:608 * W // 640] = 1  # NYU valid region
-    gt = gt * valid
-    return img.to(device), gt.to(device)
-
-
-def build(args, device):
-    from mdemi.train import FusedAdamW, SILogLoss
-    cfg = WORKLOADS[args.model]
-    torch.manual_seed(0)
-    if args.model == "adabins":
-        from mdemi.model.Adabins import UnetAdaptiveBins
-        model = UnetAdaptiveBins.build(256, 1e-3, cfg["max_depth"])
-    elif args.model == "depthformer":
-        from mdemi.model.Depthformer import DepthformerV8
-        model = DepthformerV8.build(DFV8_OPT, 1e-3, cfg["max_depth"])
+    if data_type == "NYU":
+        gt = torch.rand(B, 1, H, W, generator=g) * 9.5 + 0.5
+        valid = torch.zeros(B, 1, H, W)
+        valid[:, :, 45 * H // 480:472 * H // 480, 43 * W // 640:608 * W // 640] = 1  # NYU valid region
     else:
-        from mdemi.model.NewCRFs import NewCRFDepth
-        model = NewCRFDepth(version="large07", inv_depth=False, max_depth=cfg["max_depth"])
-    model = model.to(device).train()
-    opt = FusedAdamW(model.parameters(), lr=cfg.get("lr", 2e-5), weight_decay=cfg.get("wd", 0.0), max_grad_norm=0.1)
-    silog = SILogLoss(alpha=10.0, beta=cfg.get("beta", 0.15), per_image=cfg.get("per_image", False), min_depth=1e-3)
-    return model, opt, TrainLoss(silog, cfg.get("chamfer", 0.0), from_edges=(args.model == "adabins"))
+        gt = torch.rand(B, 1, H, W, generator=g) * 79.0 + 1.0
+        valid = (torch.rand(B, 1, H, W, generator=g) < 0.15).float()
+    return img.to(device), (gt * valid).to(device)
 
 
-class TrainLoss:
-    """SILog on the depth (+ chamfer_weight x the bin chamfer loss on AdaBins' edges / Depthformer's
-    centres when the config sets loss.chamfer_weight)."""
-
-    def __init__(self, silog, chamfer_weight, from_edges):
-        from mdemi.train import BinsChamferLoss
-        self.silog, self.w = silog, float(chamfer_weight)
-        self.chamfer = BinsChamferLoss(1e-3, from_edges=from_edges) if self.w > 0 else None
-
-    def __call__(self, out, gt):
-        pred = out[0] if isinstance(out, tuple) else out  # AdaBins / Depthformer: (depth at H/2, bins, ...)
-        loss = self.silog(pred, gt)  # SILogLoss upsamples a half-resolution prediction to the GT first
-        if self.chamfer is not None:
-            loss = loss + self.w * self.chamfer(out[1], gt)
-        return loss
-
-
-def train_step(model, opt, loss_fn, img, gt, ddp=None):
-    loss = loss_fn(model(img), gt)
-    loss.backward()
-    if ddp is not None:
-        ddp.finish()
-    opt.step()
-    opt.zero_grad(set_to_none=True)
-    return loss
+# --------------------------------------------------------------------------- roofline
+def _gemm_alg_bytes(A, B, M, N, K, kw):
+    """Algorithmic HBM bytes of one GEMM launch: every operand read once, C written once
+    (conv operands: the NHWC activation, not its im2col)."""
+    def operand(layout, rows, cols):
+        if layout == 2:  # implicit im2col: the activation tensor
+            g = kw["conv"]
+            return 4.0 * g.n * g.h * g.w * g.c
+        return 4.0 * rows * cols
+    batch = kw.get("batch", 1)
+    b = operand(kw.get("a_layout"), M, K) + operand(kw.get("b_layout"), K, N)
+    b *= batch if kw.get("a_layout") != 2 else 1
+    c = 4.0 * M * N * batch
+    b += c * (2 if kw.get("beta", 0.0) else 1)
+    for extra in ("aux", "residual", "preact"):
+        if kw.get(extra) is not None:
+            b += c
+    return b
 
 
-def gemm_roofline(model, opt, loss_fn, img, gt, ddp):
+def gemm_roofline(trainer, batches):
     """One instrumented step: HIP events around every libmdemi GEMM launch on its stream;
-    algorithmic FLOPs (2*M*N*K per GEMM) / measured kernel time, grouped by kernel."""
+    algorithmic FLOPs (2*M*N*K per GEMM) and bytes / measured kernel time, per kernel family."""
     from mdemi import functional as mf
     recs = []
     orig = mf.gemm
@@ -151,29 +187,27 @@ def gemm_roofline(model, opt, loss_fn, img, gt, ddp):
         out = orig(A, B, C, M, N, K, **kw)
         e.record(torch.cuda.current_stream())
         key = (kw.get("a_layout"), kw.get("b_layout"), kw.get("a_op", 0), kw.get("b_op", 0))
-        recs.append((key, 2.0 * M * N * K * kw.get("batch", 1), s, e))
+        recs.append((key, 2.0 * M * N * K * kw.get("batch", 1), _gemm_alg_bytes(A, B, M, N, K, kw), s, e))
         return out
 
     mf.gemm = timed
     try:
-        train_step(model, opt, loss_fn, img, gt, ddp)
+        trainer.step(batches)
         torch.cuda.synchronize()
     finally:
         mf.gemm = orig
     by = {}
-    for key, fl, s, e in recs:
+    for key, fl, by_alg, s, e in recs:
         t = s.elapsed_time(e) * 1e-3
-        a = by.setdefault(key, [0.0, 0.0, 0])
+        a = by.setdefault(key, [0.0, 0.0, 0, 0.0])
         a[0] += fl
         a[1] += t
         a[2] += 1
+        a[3] += by_alg
     tot_fl = sum(v[0] for v in by.values())
     tot_t = sum(v[1] for v in by.values())
     dom = max(by.items(), key=lambda kv: kv[1][1])
     return by, dom, tot_fl, tot_t
-
-
-KERNEL_NAME = {0: "KCONTIG", 1: "MNCONTIG", 2: "CONV"}
 
 
 def profiled_traffic(regex, workload):
@@ -186,88 +220,120 @@ def profiled_traffic(regex, workload):
     return None if fam is None else fam.get("traffic_bytes_per_launch")
 
 
-def cpu_baseline(model, name, H, W, budget_s):
+def roofline_entry(trainer, batches, workload_key, ms):
+    by, dom, tot_fl, tot_t = gemm_roofline(trainer, batches)
+    (al, bl, aop, bop), (fl, t, cnt, alg) = dom
+    ach = fl / t / 1e12
+    regex = f"gemm_f32_kernel<{al}, {bl}, {aop}, {bop},"
+    traffic = profiled_traffic(regex, workload_key)
+    alg_pl = alg / cnt
+    roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
+            "algorithmic_bytes": round(alg_pl), "traffic_over_algorithmic":
+                (round(traffic / alg_pl, 3) if traffic else None),
+            "kernel": f"gemm_f32_kernel<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}> (all pipelining variants)",
+            "kernel_regex": regex, "launches": cnt, "avg_launch_us": round(t / cnt * 1e6, 2),
+            "flops_per_launch": fl / cnt}
+    fams = {f"{KERNEL_NAME[k[0]]},{KERNEL_NAME[k[1]]},{k[2]},{k[3]}": {
+        "launches": v[2], "ms_per_step": round(v[1] * 1e3, 3), "tflops": round(v[0] / v[1] / 1e12, 2),
+        "algorithmic_GBps": round(v[3] / v[1] / 1e9, 1)} for k, v in sorted(by.items(), key=lambda kv: -kv[1][1])}
+    extra = {"gemm_all": {"achieved_tflops": round(tot_fl / tot_t / 1e12, 2), "gemm_ms_per_step": round(tot_t * 1e3, 2),
+                          "gemm_tflop_per_step": round(tot_fl / 1e12, 3),
+                          "frac": round(tot_fl / tot_t / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4), "families": fams},
+             "step_mfma_frac": round(tot_fl / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
+    return roof, extra
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(model, opt, H, W, budget_s):
     """The oracle (CPU restatement of the reference path: oracle/newcrfs.py, oracle/adabins.py,
-    oracle/depthformer.py) timed on the host cores: fp32 forward + SILog + backward + clipped AdamW
-    step at batch 1, same weights."""
+    oracle/depthformer.py) timed on the host cores: fp32 forward + loss + backward + clipped
+    AdamW step at batch 1 with the same weights, 2 warm-up steps, then as many timed steps
+    (1-5) as fit the budget."""
     from oracle import metrics as omet
-    cfg = WORKLOADS[name]
-    threads = torch.get_num_threads()
+    name = opt["model"]["name"]
+    lo = opt["loss"]
+    dmin, dmax = opt["eval"]["min_depth_eval"], opt["eval"]["max_depth_eval"]
+    threads = min(CPU_SHARE_PER_GPU, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
     P = {k: v.detach().float().cpu().clone().requires_grad_(torch.is_floating_point(v))
          for k, v in model.state_dict().items()}
     params = [v for v in P.values() if v.requires_grad]
-    opt = torch.optim.AdamW(params, lr=cfg.get("lr", 2e-5), weight_decay=cfg.get("wd", 0.0))
-    img, gt = synthetic_batch(1, H, W, "cpu", seed=1)
+    copt = torch.optim.AdamW(params, lr=opt["optimizer"]["lr"], weight_decay=opt["optimizer"]["weight_decay"])
+    img, gt = synthetic_batch(1, H, W, "cpu", seed=1, data_type=opt["dataset"]["data_type"])
     if name == "adabins":
         from oracle import adabins as oab
-        fwd = lambda: oab.unet_adaptive_bins(P, img, 1e-3, cfg["max_depth"])  # noqa: E731
-    elif name == "depthformer":
+        fwd = lambda: oab.unet_adaptive_bins(P, img, dmin, dmax)  # noqa: E731
+    elif name == "depthformer_v8":
         from oracle import depthformer as odf
-        opt_m = dict(DFV8_OPT, attn_drop_prob=0.0, drop_prob=0.0)
-        fwd = lambda: odf.depthformer_v8_full(P, img, opt_m, 1e-3, cfg["max_depth"])  # noqa: E731
+        opt_m = dict(opt["model"], attn_drop_prob=0.0, drop_prob=0.0)
+        fwd = lambda: odf.depthformer_v8_full(P, img, opt_m, dmin, dmax)  # noqa: E731
     else:
         from oracle import newcrfs as onc
-        fwd = lambda: onc.newcrf_depth(P, img, "large07", max_depth=cfg["max_depth"])  # noqa: E731
+        fwd = lambda: onc.newcrf_depth(P, img, "large07", max_depth=dmax)  # noqa: E731
+    cham = float(lo.get("chamfer_weight", 0.0))
 
     def step():
         out = fwd()
         pred = out[0] if isinstance(out, tuple) else out
         if pred.shape[-2:] != gt.shape[-2:]:
             pred = torch.nn.functional.interpolate(pred, gt.shape[-2:], mode="bilinear", align_corners=True)
-        loss = omet.silog_loss(pred, gt, 1e-3, 10.0, cfg.get("beta", 0.15), cfg.get("per_image", False))
-        if cfg.get("chamfer", 0.0) > 0:
+        loss = omet.silog_loss(pred, gt, dmin, lo["alpha"], lo["beta"], lo["per_image"])
+        if cham > 0:
             from oracle.adabins import bins_chamfer_loss
-            loss = loss + cfg["chamfer"] * bins_chamfer_loss(out[1], gt, 1e-3, from_edges=(name == "adabins"))
+            loss = loss + cham * bins_chamfer_loss(out[1], gt, dmin, from_edges=(name == "adabins"))
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(params, 0.1)
-        opt.step()
-        opt.zero_grad(set_to_none=True)
+        torch.nn.utils.clip_grad_norm_(params, opt["train"]["grad_norm"])
+        copt.step()
+        copt.zero_grad(set_to_none=True)
 
     t0 = time.perf_counter()
-    step()  # warm-up
-    first = time.perf_counter() - t0
-    n = max(1, min(5, int(budget_s / max(first, 1e-3))))
+    step()
+    step()  # 2 warm-up steps
+    per = (time.perf_counter() - t0) / 2
+    n = max(1, min(5, int(budget_s / max(per, 1e-3))))
     t0 = time.perf_counter()
     for _ in range(n):
         step()
     dt = (time.perf_counter() - t0) / n
     return {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle {cfg['model']} fp32 train step (fwd+SILog{'+chamfer' if cfg.get('chamfer') else ''}+bwd+AdamW), batch 1 at {H}x{W}, "
-                      f"{n} timed steps after 1 warm-up, {threads} threads, {os.cpu_count()} host CPUs visible"}
+            "sample": f"oracle {name} fp32 train step (fwd+SILog{'+chamfer' if cham else ''}+bwd+clip+AdamW), "
+                      f"batch 1 at {H}x{W}, {n} timed steps after 2 warm-up, {threads} threads (the box's "
+                      f"per-GPU CPU share), {os.cpu_count()} host CPUs visible, CPU: {_cpu_model()}"}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
-    cfg = WORKLOADS[args.model]
-    B = args.batch or cfg["batch"]
-    H = args.height or cfg["h"]
-    W = args.width or cfg["w"]
-
-    model, opt, loss_fn = build(args, device)
-    ddp = None
-    if world > 1:  # bucketed RCCL gradient mean overlapped with backward (mdemi/train/ddp.py)
-        from mdemi.train import GradAllReduce, broadcast_parameters
-        broadcast_parameters(model)  # identical replicas (DDP broadcasts rank 0's weights)
-        ddp = GradAllReduce(model, bucket_mb=64.0)
-    img, gt = synthetic_batch(B, H, W, device, seed=1000 + rank)
-
+# --------------------------------------------------------------------------- one measurement
+def measure(args, opt, key, H, W, B, rank, world, device, with_roofline):
+    """Build the trainer from `opt`, run W warm-up + K timed steps; returns a dict."""
+    from mdemi.train import build_from_config
+    opt = copy.deepcopy(opt)
+    opt["dataloader"]["batch_size"] = B
+    torch.manual_seed(0)
+    trainer = build_from_config(opt, device=device, world=world)
+    na = trainer.num_accum
+    batches = [synthetic_batch(B, H, W, device, seed=1000 + 7 * rank + i, data_type=opt["dataset"]["data_type"])
+               for i in range(na)]
     for _ in range(args.warmup):
-        train_step(model, opt, loss_fn, img, gt, ddp)
+        trainer.step(batches)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = train_step(model, opt, loss_fn, img, gt, ddp)
+        loss = trainer.step(batches)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -277,44 +343,167 @@ def main():
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    loss_v = float(loss.item())
-    ms = elapsed / args.steps * 1e3
-    value = B * world * args.steps / elapsed
+    res = {"elapsed": elapsed, "ms": elapsed / args.steps * 1e3, "images": B * na * world * args.steps,
+           "loss": float(loss.item()), "num_accum": na, "trainer": trainer}
+    if world > 1:  # isolated cost of the whole gradient exchange (no overlap): an upper bound on exposed comm
+        ddp = trainer.ddp
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            ddp.allreduce_all()
+        torch.cuda.synchronize()
+        iso = (time.perf_counter() - t0) / 3 * 1e3
+        res["allreduce"] = {"grad_bytes": sum(ddp.bucket_bytes), "buckets": len(ddp.buckets),
+                            "isolated_ms": round(iso, 2), "share_of_step_upper_bound": round(iso / res["ms"], 4),
+                            "bus_GBps": round(2 * (world - 1) / world * sum(ddp.bucket_bytes) / (iso * 1e-3) / 1e9, 1)}
+    if with_roofline:
+        res["roofline"], res["extra"] = roofline_entry(trainer, batches, key, res["ms"])
+    return res
 
-    roof = None
-    extra = {}
-    if not args.no_roofline:
-        by, dom, tot_fl, tot_t = gemm_roofline(model, opt, loss_fn, img, gt, ddp)
-        (al, bl, aop, bop), (fl, t, cnt) = dom
-        ach = fl / t / 1e12
-        regex = f"gemm_f32_kernel<{al}, {bl}, {aop}, {bop},"
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": profiled_traffic(regex, args.model), "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
-                "kernel": f"gemm_f32_kernel<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}> (all pipelining variants)",
-                "kernel_regex": regex, "launches": cnt, "avg_launch_us": round(t / cnt * 1e6, 2),
-                "flops_per_launch": fl / cnt}
-        extra["gemm_all"] = {"achieved_tflops": round(tot_fl / tot_t / 1e12, 2), "gemm_ms_per_step": round(tot_t * 1e3, 2),
-                             "gemm_tflop_per_step": round(tot_fl / 1e12, 3),
-                             "frac": round(tot_fl / tot_t / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
-        extra["step_mfma_frac"] = round(tot_fl / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)
 
+# --------------------------------------------------------------------------- plumbing (CPU)
+def plumbing_main(args, rank, world):
+    """--device cpu: the launcher / gloo / barrier / max-over-ranks / JSON path with a toy
+    model (no libmdemi); for the CPU tests of the N > 1 launch only."""
+    from mdemi.train.ddp import GradAllReduce, broadcast_parameters
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 1))
+    ddp = None
+    if world > 1:
+        broadcast_parameters(model)
+        ddp = GradAllReduce(model, bucket_mb=0.0002)
+    optim = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    x = torch.randn(8, 32, generator=torch.Generator().manual_seed(rank))
+
+    def step():
+        loss = model(x).square().mean()
+        loss.backward()
+        if ddp is not None:
+            ddp.finish()
+        optim.step()
+        if ddp is not None:
+            ddp.zero_grad()
+        else:
+            optim.zero_grad()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        with torch.no_grad():
+            psum = torch.stack([p.detach().double().sum() for p in model.parameters()]).sum()
+        lo_hi = torch.stack([-psum, psum])
+        dist.all_reduce(lo_hi, op=dist.ReduceOp.MAX)
+        identical = bool(-lo_hi[0] == lo_hi[1])
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing (CPU toy model; not a measurement)", "value": 8 * world * args.steps /
+                          elapsed, "unit": "samples/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "data": "plumbing", "config": {"workload": "plumbing", "parallelism": f"dp{world}"},
+                          "buckets": len(ddp.buckets) if ddp else 0,
+                          "launch_order": ddp.last_launch_order if ddp else [],
+                          "replicas_identical": identical if world > 1 else True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.device == "cpu":
+        return plumbing_main(args, rank, world)
+    if local >= torch.cuda.device_count():
+        print(f"bench: local rank {local} has no GPU ({torch.cuda.device_count()} visible)", file=sys.stderr)
+        sys.exit(2)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
+    device = torch.device("cuda", local)
+
+    if args.config:
+        with open(args.config) as f:
+            opt = json.load(f)
+        key, ref_cfg = "config", args.config
+        img = opt.get("dataset", {}).get("img_size")
+        dt = opt.get("dataset", {}).get("data_type", "NYU")
+        H, W = (args.height or (img[0] if img else (480 if dt == "NYU" else 352)),
+                args.width or (img[1] if img else (640 if dt == "NYU" else 704)))
+        wl = dict(model=opt["model"]["name"], workload=f"{opt['model']['name']} train step from {args.config}")
+    else:
+        key = args.model
+        wl = WORKLOADS[key]
+        opt, ref_cfg = wl["opt"], wl["ref_cfg"]
+        H, W = args.height or wl["h"], args.width or wl["w"]
+    B = args.batch or int(opt["dataloader"]["batch_size"])
+
+    res = measure(args, opt, key, H, W, B, rank, world, device, with_roofline=not args.no_roofline)
+    value = res["images"] / res["elapsed"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(model, args.model, H, W, args.cpu_budget_s)
+        cpu = cpu_baseline(res["trainer"].model, opt, H, W, args.cpu_budget_s)
+    del res["trainer"]
+    torch.cuda.empty_cache()
+
+    secondary = None
+    if key == "newcrfs" and not args.no_secondary and args.batch is None and args.height is None:
+        wk = WORKLOADS["newcrfs_kitti"]
+        sec = measure(args, wk["opt"], "newcrfs_kitti", wk["h"], wk["w"], 8, rank, world, device,
+                      with_roofline=not args.no_roofline)
+        del sec["trainer"]
+        secondary = {"workload": wk["workload"], "reference_config": wk["ref_cfg"], "per_gpu_batch": 8,
+                     "images_per_sec": round(sec["images"] / sec["elapsed"], 3), "ms_per_step": round(sec["ms"], 2),
+                     "loss": round(sec["loss"], 5)}
+        if "roofline" in sec:
+            secondary["roofline"] = sec["roofline"]
+            secondary["step_mfma_frac"] = sec["extra"]["step_mfma_frac"]
+            # SURVEY §8d: 2404.7 GFLOP per image per train step at 352x1216 (reference flop count)
+            secondary["survey_flop_frac"] = round(2404.7e9 * sec["images"] / sec["elapsed"] / world / 1e12 /
+                                                  FP32_MFMA_PEAK_TFLOPS, 4)
+        if "allreduce" in sec:
+            secondary["allreduce"] = sec["allreduce"]
 
     if rank == 0:
         line = {
-            "metric": ("images/sec (train step) NYU 640x480 bs=8/GPU" if args.model == "newcrfs" else
-                       f"images/sec (train step) {cfg['model']} {W}x{H} bs={B}/GPU"),
+            "metric": ("images/sec (train step) NYU 640x480 bs=8/GPU" if key == "newcrfs" else
+                       f"images/sec (train step) {wl['model']} {W}x{H} bs={B}/GPU"),
             "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": round(res["ms"], 2), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights)",
-            "config": {"workload": cfg["workload"], "model": cfg["model"], "global_batch": B * world,
-                       "per_gpu_batch": B, "image": [H, W], "parallelism": f"dp{world}",
-                       "reference_config": cfg["ref_cfg"]},
-            "roofline": roof, "cpu_baseline": cpu, "loss": round(loss_v, 5), **extra,
+            "config": {"workload": wl["workload"], "model": wl["model"], "global_batch": B * world,
+                       "per_gpu_batch": B, "num_accum": res["num_accum"], "image": [H, W],
+                       "parallelism": f"dp{world}", "reference_config": ref_cfg},
+            "roofline": res.get("roofline"), "cpu_baseline": cpu, "loss": round(res["loss"], 5),
+            "rccl_world": world if world > 1 else None,
         }
+        if "allreduce" in res:
+            line["allreduce"] = res["allreduce"]
+        line.update(res.get("extra", {}))
+        if secondary is not None:
+            line["secondary"] = secondary
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -204,7 +204,7 @@ class SwinTransformer(nn.Module):
         self.patch_embed = PatchEmbed(patch_size=patch_size, in_chans=in_chans, embed_dim=embed_dim,
                                       norm_layer=norm_layer if patch_norm else None)
         self.pos_drop = nn.Dropout(p=drop_rate)
-        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths))]
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths), device="cpu")]
         self.layers = nn.ModuleList()
         for i in range(self.num_layers):
             self.layers.append(BasicLayer(

@@ -6,3 +6,4 @@ choices are documented in DESIGN.md."""
 from .optim import FusedAdamW, OneCycleLR  # noqa: F401
 from .loss import BinsChamferLoss, SILogLoss  # noqa: F401
 from .ddp import GradAllReduce, broadcast_parameters  # noqa: F401
+from .builder import Trainer, TrainLoss, build_from_config  # noqa: F401

@@ -1,0 +1,221 @@
+"""Config-driven train step: the restated run.py's construction phase.
+
+The reference snapshot has no run.py (evidence
+output/test/wandb/latest-run/files/wandb-metadata.json:16 and the traceback
+in run-1pklfwui.wandb), but its JSON configs (json/{nyu,kitti,online}/**)
+name every choice the train step makes.  ``build_from_config(opt)`` maps an
+``opt`` as returned by ``utils.common_utils.parse`` (common_utils.py:34-52),
+unchanged, onto this framework's objects:
+
+  model.name            adabins        -> UnetAdaptiveBins.build(num_bins, min, max)   unet_adaptive_bins.py:126-139
+                        newcrfs        -> NewCRFDepth('large07', max_depth=max)        NewCRFDepth.py:15
+                        depthformer_v8 -> DepthformerV8.build(opt.model, min, max)      depthformer_v8.py:84-102
+  model.bn_momentum     -> every BatchNorm's momentum
+  loss.alpha/beta/per_image -> SILogLoss (+ loss.chamfer_weight x BinsChamferLoss on the bins)
+  optimizer.lr/weight_decay/betas/eps/same_lr -> FusedAdamW; with get_1x_lr_params
+                        (unet_adaptive_bins.py:111-117) and same_lr false: two groups,
+                        encoder at lr/10, the rest at lr
+  scheduler.name=onecycle, pct_start/div_factor/final_div_factor/cycle_momentum
+                        -> OneCycleLR (max_lr = each group's lr; total = epoch x
+                           optimizer steps per epoch)
+  train.grad_norm       -> global-norm clip folded into the AdamW step
+  train.num_accum       -> micro-steps accumulated per optimizer step (DDP no_sync
+                           on all but the last)
+  train.freeze_encoder_bn / freeze_all_bn -> BatchNorm modules kept in eval mode
+                           (common_utils.py:78-81 freeze_bn)
+  eval.min/max_depth_eval -> the model's depth range (NYU 10 m, KITTI 80 m)
+
+What is a decision rather than parity (the reference does not pin it) is
+listed in DESIGN.md §1 (restated train step).  The depth range follows
+upstream AdaBins / NeW-CRFs (min 1e-3, max = the dataset's max_depth_eval)."""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .loss import BinsChamferLoss, SILogLoss
+from .optim import FusedAdamW, OneCycleLR
+
+MODEL_NAMES = ("adabins", "newcrfs", "depthformer_v8")
+# training-split sizes behind the default steps-per-epoch: depth_dataset.py:79 reads
+# train_test_inputs/NYU/nyu_train_36k.txt (36,253 pairs), :49 KITTI/kitti_eigen_train.txt
+# (23,158); ONLINE's kitti_benchmark_train.txt is a missing blob, so KITTI's count stands in
+TRAIN_IMAGES = {"NYU": 36253, "KITTI": 23158, "ONLINE": 23158}
+
+
+def _depth_range(opt):
+    ev = opt.get("eval", {})
+    return float(ev.get("min_depth_eval", 1e-3)), float(ev.get("max_depth_eval", 10.0))
+
+
+def build_model(opt, drop_path=None):
+    m = opt["model"]
+    name = m["name"]
+    dmin, dmax = _depth_range(opt)
+    if name == "adabins":
+        from ..model.Adabins import UnetAdaptiveBins
+        model = UnetAdaptiveBins.build(int(m.get("num_bins", 256)), dmin, dmax)
+    elif name == "newcrfs":
+        from ..model.NewCRFs import NewCRFDepth
+        kw = {} if drop_path is None else {"drop_path_rate": drop_path}
+        model = NewCRFDepth(version=m.get("version", "large07"), inv_depth=False, max_depth=dmax, **kw)
+    elif name == "depthformer_v8":
+        from ..model.Depthformer import DepthformerV8
+        model = DepthformerV8.build(m, dmin, dmax)
+    else:
+        raise ValueError(f"model.name {name!r} is not on this framework's path (one of {MODEL_NAMES})")
+    if "bn_momentum" in m:
+        for mod in model.modules():
+            if isinstance(mod, nn.modules.batchnorm._BatchNorm):
+                mod.momentum = float(m["bn_momentum"])
+    return model
+
+
+class TrainLoss:
+    """SILog on the depth (+ chamfer_weight x the bin chamfer loss on AdaBins' edges /
+    Depthformer's centres when loss.chamfer_weight > 0)."""
+
+    def __init__(self, opt, model_name):
+        lo = opt.get("loss", {})
+        dmin, _ = _depth_range(opt)
+        self.silog = SILogLoss(alpha=float(lo.get("alpha", 10.0)), beta=float(lo.get("beta", 0.15)),
+                               per_image=bool(lo.get("per_image", False)), min_depth=dmin)
+        self.w = float(lo.get("chamfer_weight", 0.0))
+        self.chamfer = BinsChamferLoss(dmin, from_edges=(model_name == "adabins")) if self.w > 0 else None
+
+    def __call__(self, out, gt):
+        pred = out[0] if isinstance(out, tuple) else out
+        loss = self.silog(pred, gt)  # SILogLoss upsamples a half-resolution prediction to the GT first
+        if self.chamfer is not None:
+            loss = loss + self.w * self.chamfer(out[1], gt)
+        return loss
+
+
+def param_groups(model, opt):
+    o = opt.get("optimizer", {})
+    lr = float(o["lr"])
+    same_lr = bool(o.get("same_lr", False))
+    if not same_lr and hasattr(model, "get_1x_lr_params"):
+        return [{"params": list(model.get_1x_lr_params()), "lr": lr / 10.0},
+                {"params": list(model.get_10x_lr_params()), "lr": lr}]
+    return [{"params": list(model.parameters()), "lr": lr}]
+
+
+def build_optimizer(model, opt):
+    o = opt.get("optimizer", {})
+    betas = tuple(float(b) for b in o.get("betas", (0.9, 0.999)))
+    return FusedAdamW(param_groups(model, opt), lr=float(o["lr"]), betas=betas, eps=float(o.get("eps", 1e-8)),
+                      weight_decay=float(o.get("weight_decay", 0.0)),
+                      max_grad_norm=float(opt.get("train", {}).get("grad_norm", 0.0)))
+
+
+def optimizer_steps_per_epoch(opt, world=1, images=None):
+    data_type = opt.get("dataset", {}).get("data_type", "NYU")
+    images = images if images is not None else TRAIN_IMAGES.get(data_type, 36253)
+    batch = int(opt.get("dataloader", {}).get("batch_size", 8))
+    loader_len = math.ceil(images / (batch * world))
+    return max(1, loader_len // int(opt.get("train", {}).get("num_accum", 1)))
+
+
+def build_scheduler(optimizer, opt, steps_per_epoch):
+    s = opt.get("scheduler", {})
+    name = s.get("name", "onecycle")
+    if name != "onecycle":
+        raise ValueError(f"scheduler.name {name!r}: only 'onecycle' is configured by the reference")
+    total = int(opt.get("train", {}).get("epoch", 1)) * int(steps_per_epoch)
+    return OneCycleLR(optimizer, max_lr=[g["lr"] for g in optimizer.param_groups], total_steps=total,
+                      pct_start=float(s.get("pct_start", 0.3)), div_factor=float(s.get("div_factor", 25.0)),
+                      final_div_factor=float(s.get("final_div_factor", 1e4)),
+                      cycle_momentum=bool(s.get("cycle_momentum", True)))
+
+
+def freeze_bn(model):
+    """common_utils.py:78-81."""
+    for m in model.modules():
+        if isinstance(m, nn.modules.batchnorm._BatchNorm):
+            m.eval()
+
+
+class Trainer:
+    """One optimizer step = num_accum micro-batches of forward + loss/num_accum + backward
+    (gradients accumulate in place), then the gradient all-reduce (DDP), the clipped
+    AdamW update and one OneCycle step."""
+
+    def __init__(self, opt, model, criterion, optimizer, scheduler, ddp=None):
+        tr = opt.get("train", {})
+        self.opt, self.model, self.criterion = opt, model, criterion
+        self.optimizer, self.scheduler, self.ddp = optimizer, scheduler, ddp
+        self.num_accum = int(tr.get("num_accum", 1))
+        self.freeze_encoder_bn = bool(tr.get("freeze_encoder_bn", False))
+        self.freeze_all_bn = int(tr.get("freeze_all_bn", -1))
+        self.epoch = 0
+
+    def train_mode(self):
+        self.model.train()
+        enc = getattr(self.model, "encoder", None)
+        if self.freeze_encoder_bn and enc is not None:
+            freeze_bn(enc)
+        if 0 <= self.freeze_all_bn <= self.epoch:
+            freeze_bn(self.model)
+
+    def step(self, batches):
+        """batches: num_accum (image, gt) pairs; returns the summed (scaled) loss tensor."""
+        if len(batches) != self.num_accum:
+            raise ValueError(f"Trainer.step: expected {self.num_accum} micro-batches (train.num_accum), "
+                             f"got {len(batches)}")
+        total = None
+        for i, (img, gt) in enumerate(batches):
+            last = i == len(batches) - 1
+            ctx = self.ddp.no_sync() if (self.ddp is not None and not last) else _null()
+            with ctx:
+                loss = self.criterion(self.model(img), gt)
+                if self.num_accum > 1:
+                    loss = loss * (1.0 / self.num_accum)
+                loss.backward()
+            total = loss.detach() if total is None else total + loss.detach()
+        if self.ddp is not None:
+            self.ddp.finish()
+        self.optimizer.step()
+        if self.scheduler is not None:
+            self.scheduler.step()
+        if self.ddp is not None:
+            self.ddp.zero_grad()
+        else:
+            self.optimizer.zero_grad(set_to_none=True)
+        return total
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def build_from_config(opt, device=None, world=1, steps_per_epoch=None, ddp_bucket_mb=64.0, drop_path=None):
+    """opt (parse()'s dict) -> Trainer.  device='meta' builds every object without
+    allocating parameters (config validation); world > 1 wraps the gradients in the
+    bucketed RCCL all-reduce (needs an initialised process group)."""
+    name = opt["model"]["name"]
+    if device is not None and torch.device(device).type == "meta":
+        with torch.device("meta"):
+            model = build_model(opt, drop_path)
+    else:
+        model = build_model(opt, drop_path)
+        if device is not None:
+            model = model.to(device)
+    criterion = TrainLoss(opt, name)
+    optimizer = build_optimizer(model, opt)
+    spe = steps_per_epoch if steps_per_epoch is not None else optimizer_steps_per_epoch(opt, world)
+    scheduler = build_scheduler(optimizer, opt, spe)
+    ddp = None
+    if world > 1:
+        from .ddp import GradAllReduce, broadcast_parameters
+        broadcast_parameters(model)
+        ddp = GradAllReduce(model, bucket_mb=ddp_bucket_mb)
+    trainer = Trainer(opt, model, criterion, optimizer, scheduler, ddp)
+    trainer.train_mode()
+    return trainer

@@ -3,15 +3,32 @@ DistributedDataParallel inside the missing run.py; evidence
 utils/common_utils.py:20-21).  One process per GPU; the only exchange step of
 a train step is the mean of every parameter gradient across ranks.
 
-GradAllReduce packs gradients into ~bucket_mb buckets in reverse registration
-order (the order backward produces them), and launches each bucket's
-all-reduce from a post-accumulate-grad hook as soon as its last gradient
-lands, so RCCL (torch.distributed "nccl" == RCCL over xGMI on ROCm) overlaps
-the rest of the backward.  finish() waits for the outstanding collectives and
-scatters bucket / world back into the .grad tensors.  The pack / unpack
-sweeps are libmdemi kernels (copy2d / AXPBY); the CPU gloo tests swap them
-for torch ops through the two hooks below, nothing else changes."""
+Layout.  Parameters are grouped into ~bucket_mb buckets in reverse
+registration order (the order backward produces their gradients).  Each
+bucket is ONE persistent flat fp32 buffer, allocated once, and every
+parameter's ``.grad`` is a view into its bucket (DDP's
+``gradient_as_bucket_view``): autograd accumulates straight into the bucket,
+so there is no pack and no unpack sweep, gradient accumulation over
+``train.num_accum`` micro-steps happens in place, and the optimizer and a
+captured hipGraph see the same gradient addresses every step.
+
+Protocol.  A post-accumulate-grad hook counts the gradients that landed in
+each bucket; a bucket is ready when all of them have.  Buckets are launched
+strictly in index order (bucket i waits until buckets 0..i-1 have launched),
+so every rank issues the same sequence of collectives whatever order its
+autograd engine fires hooks in.  Each launch is an async all-reduce (SUM) on
+torch.distributed's communication stream — backend "nccl" is RCCL over xGMI
+on ROCm — overlapping the rest of the backward.  ``finish()`` waits for the
+outstanding collectives and scales each bucket by 1/world in place (one
+libmdemi sweep per bucket).  Inside ``no_sync()`` the hooks only let
+gradients accumulate; the reduction happens on the first backward outside it.
+
+If something replaced a ``.grad`` (``zero_grad(set_to_none=True)``, a first
+step before the views were installed), the hook copies it into the bucket
+slice and re-installs the view, so the protocol stays correct."""
 from __future__ import annotations
+
+import contextlib
 
 import torch
 import torch.distributed as dist
@@ -22,6 +39,12 @@ class GradAllReduce:
         self.group = group
         self.world = dist.get_world_size(group)
         self.params = [p for p in model.parameters() if p.requires_grad]
+        if not self.params:
+            raise ValueError("GradAllReduce: model has no trainable parameters")
+        dtype = self.params[0].dtype
+        dev = self.params[0].device
+        if any(p.dtype != dtype or p.device != dev for p in self.params):
+            raise ValueError("GradAllReduce: all parameters must share one dtype and device")
         self.buckets, cur, size = [], [], 0
         for p in reversed(self.params):
             cur.append(p)
@@ -31,55 +54,121 @@ class GradAllReduce:
                 cur, size = [], 0
         if cur:
             self.buckets.append(cur)
-        self.bucket_of = {p: bi for bi, b in enumerate(self.buckets) for p in b}
+        self.bucket_of, self.slot = {}, {}
+        self.flat = []
+        for bi, b in enumerate(self.buckets):
+            n = sum(p.numel() for p in b)
+            flat = torch.zeros(n, dtype=dtype, device=dev)
+            self.flat.append(flat)
+            off = 0
+            for p in b:
+                self.bucket_of[p] = bi
+                self.slot[p] = (off, p.numel())
+                off += p.numel()
+        self.bucket_bytes = [f.numel() * f.element_size() for f in self.flat]
+        self._install_views(copy_existing=True)
         self.launch_order: list[int] = []
-        self._flat = [None] * len(self.buckets)
+        self.last_launch_order: list[int] = []
         self._works = []
+        self._sync = True
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
         self.reset()
 
-    # ---- pack / unpack (libmdemi sweeps on the GPU) ----
-    def _flatten(self, grads):
-        from .. import functional as mf
-        return mf.concat_channels([g.reshape(1, -1) for g in grads]).view(-1)
+    # ---- gradient storage ----
+    def _view(self, p):
+        off, n = self.slot[p]
+        return self.flat[self.bucket_of[p]][off:off + n].view_as(p)
 
-    def _unflatten_mean(self, flat, grads):
-        from .. import _lib as L
-        off = 0
-        for g in grads:
-            n = g.numel()
-            L.call("mdemi_elementwise", L.EW_AXPBY, flat[off:off + n].data_ptr(), flat[off:off + n].data_ptr(),
-                   g.data_ptr(), n, 1.0 / self.world, 0.0, L.stream())
-            off += n
+    def _install_views(self, copy_existing=False):
+        for p in self.params:
+            v = self._view(p)
+            if copy_existing and p.grad is not None:
+                self._copy(p.grad, v)
+            p.grad = v
+
+    def _is_view(self, p):
+        g = p.grad
+        return g is not None and g.data_ptr() == self._view(p).data_ptr()
+
+    # ---- device sweeps (libmdemi on the GPU; the CPU gloo tests override these two) ----
+    def _copy(self, src, dst):
+        if src.is_cuda:
+            from .. import _lib as L
+            s = src.contiguous()
+            L.call("mdemi_elementwise", L.EW_AXPBY, s.data_ptr(), s.data_ptr(), dst.data_ptr(), s.numel(), 1.0, 0.0,
+                   L.stream())
+        else:
+            dst.copy_(src)
+
+    def _scale(self, flat, s):
+        if flat.is_cuda:
+            from .. import _lib as L
+            L.call("mdemi_elementwise", L.EW_AXPBY, flat.data_ptr(), flat.data_ptr(), flat.data_ptr(), flat.numel(),
+                   float(s), 0.0, L.stream())
+        else:
+            flat.mul_(s)
 
     # ---- protocol ----
     def reset(self):
         self._pending = [len(b) for b in self.buckets]
+        self._next = 0
         self._works = []
         self.launch_order = []
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (train.num_accum micro-steps); reduce on the next
+        backward outside this context (torch DDP's no_sync)."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
     def _hook(self, p):
+        if not self._is_view(p):  # .grad was replaced: fold it back into the bucket
+            g = p.grad
+            self._copy(g, self._view(p))
+            p.grad = self._view(p)
+        if not self._sync:
+            return
         bi = self.bucket_of[p]
         self._pending[bi] -= 1
-        if self._pending[bi] == 0:
-            grads = [q.grad for q in self.buckets[bi]]
-            flat = self._flatten(grads)
-            self._flat[bi] = (flat, grads)
+        # launch every ready bucket in index order (identical collective sequence on all ranks)
+        while self._next < len(self.buckets) and self._pending[self._next] == 0:
+            bi = self._next
             self.launch_order.append(bi)
-            self._works.append(dist.all_reduce(flat, group=self.group, async_op=True))
+            self._works.append(dist.all_reduce(self.flat[bi], group=self.group, async_op=True))
+            self._next += 1
 
     def finish(self):
+        """Wait for the bucket all-reduces and turn the sums into means (in place)."""
         if any(n != 0 for n in self._pending):
             missing = [bi for bi, n in enumerate(self._pending) if n != 0]
             raise RuntimeError(f"GradAllReduce: buckets {missing} never completed (unused parameters?)")
         for w in self._works:
             w.wait()
-        for item in self._flat:
-            if item is not None:
-                self._unflatten_mean(*item)
-        self._flat = [None] * len(self.buckets)
+        if self.world > 1:
+            for flat in self.flat:
+                self._scale(flat, 1.0 / self.world)
+        for p in self.params:  # an optimizer may have replaced a view meanwhile
+            if not self._is_view(p):
+                p.grad = self._view(p)
         self.last_launch_order = list(self.launch_order)
         self.reset()
+
+    def zero_grad(self):
+        """Zero the buckets (the gradients stay views; use instead of set_to_none)."""
+        for flat in self.flat:
+            flat.zero_()
+        for p in self.params:
+            if not self._is_view(p):
+                p.grad = self._view(p)
+
+    def allreduce_all(self):
+        """All buckets reduced back to back with no overlap (bench: isolated comm cost)."""
+        for flat in self.flat:
+            dist.all_reduce(flat, group=self.group)
 
     def remove(self):
         for h in self._handles:

@@ -1,9 +1,9 @@
 """The data-parallel gradient exchange with GPU gradients: two ranks on cuda:0
 (a one-GPU box cannot host two RCCL ranks, so the process group is gloo,
 which all-reduces CUDA tensors through the host), running the real
-GradAllReduce -- libmdemi pack (concat_channels) / unpack (AXPBY by 1/world)
-on the GPU, buckets launched from post-accumulate-grad hooks -- around a tiny
-NeW-CRFs train step.  The mean of the per-rank gradients must equal the
+GradAllReduce -- gradients as views of persistent flat buckets, buckets
+launched in index order from post-accumulate-grad hooks, the 1/world scale a
+libmdemi sweep per bucket -- around a tiny NeW-CRFs train step.  The mean of the per-rank gradients must equal the
 per-shard gradients averaged on one replica, and every rank must end with the
 same gradients.  RCCL itself only differs in the transport."""
 import os
@@ -83,11 +83,11 @@ def test_grad_allreduce_gpu_gradients_two_ranks():
     for r, v in out.items():
         assert not isinstance(v, str), f"rank {r} failed: {v}"
     assert out[0]["nbuckets"] > 2
-    assert sorted(out[0]["order"]) == list(range(out[0]["nbuckets"]))
+    assert out[0]["order"] == list(range(out[0]["nbuckets"])) == out[1]["order"]
     for r in out:
         out[r]["grads"] = [torch.from_numpy(g) for g in out[r]["grads"]]
     for a, b in zip(out[0]["grads"], out[1]["grads"]):
-        assert torch.equal(a, b)  # one all-reduced buffer, one unpack: identical on every rank
+        assert torch.equal(a, b)  # one all-reduced buffer, one scale: identical on every rank
     # single replica: per-shard gradients, averaged
     acc = None
     for r in range(world):
