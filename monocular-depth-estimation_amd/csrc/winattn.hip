@@ -98,8 +98,7 @@ struct WinParams {
   const float* dout;
   float* dq; float* dk; int64_t dqk_ld;
   float* dv; int64_t dv_ld;
-  float* partial;  // [nwin][heads][T + 2*HD]
-  float* dsum;     // [nwin][heads][N]  D_i = dO_i . O_i
+  float* partial;  // [nwin][heads][T + 2*HD]: bias-table gradient, pad-key k / v gradient sums
 };
 
 // ---------------------------------------------------------------------------
@@ -187,6 +186,16 @@ __device__ __forceinline__ void mma_tok(wa_f16x (&out)[2], const float (*rows)[W
     }
 }
 
+// Ordering of a wave's own LDS traffic (every LDS image below is private to
+// one wave): the wave's DS instructions execute in issue order, so a compiler
+// fence + wave barrier is enough -- no workgroup barrier couples the four
+// independent (window, head) items of a workgroup.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 struct WaItem {
   int item, win, hh;
   bool active;
@@ -239,7 +248,7 @@ __global__ __launch_bounds__(256) void winattn_fwd_kernel(WinParams p, const flo
     }
     mma_hd(s, kf, qf);
   }
-  __syncthreads();  // Vs, regs
+  wave_lds_sync();  // Vs, regs
   if (border) {
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
@@ -299,57 +308,77 @@ __global__ __launch_bounds__(256) void winattn_fwd_kernel(WinParams p, const flo
   }
 }
 
-// Backward, query side (lane column = query): recompute P^T, dP^T = V dO^T,
-// dS^T = P^T (dP^T - D), D = rowsum(dO o O); dQ^T = K^T dS^T; bias-table
-// gradient through per-wave LDS atomics.
+// Fused backward: one wave per (window, head), one pass over Q/K/V/O/dO.
+// In the S^T orientation of the forward (rows = keys in registers, columns =
+// queries on lanes) the wave recomputes P^T = exp(S^T - lse) and
+// dP^T = V dO^T, forms dS^T = P^T (dP^T - D) with D = rowsum(dO o O), and
+//   dQ^T[d][q]  = sum_key K[key][d] dS^T[key][q]     (contracts the register rows)
+//   dK[key][d]  = sum_q dS^T[key][q] (scale Q)[q][d] (contracts the lane columns)
+//   dV[key][d]  = sum_q P^T[key][q] dO[q][d]
+// The two products that contract over queries read the score tile back from
+// a per-wave [key][query] LDS image (pitch 65: conflict-free both ways), so
+// no score is computed twice.  The per-lane operand columns (K[key][l31],
+// Q[q][l31], dO[q][l31]) come straight from global rows (L2 hits).  The
+// relative-position-bias gradient is gathered through per-wave LDS atomics;
+// pad keys (whose k / v were the Linear bias) fold into per-item sums.
+constexpr int WA_TP = WA_NP + 1;
+
+// Column fetch for a window token through the wave's row table (rowtab[tok] =
+// the token's row, -1 for a pad token, -2 for MFMA padding): value of column
+// `col` with the forward's pad / zero semantics, branch-free.
+__device__ __forceinline__ float col_val(const float* base, int64_t ld, const float* pad, int row, int col) {
+  const float* src = row >= 0 ? base + (int64_t)row * ld + col : ((row == -1 && pad) ? pad + col : g_wa_zero + (col & 31));
+  return *src;
+}
+
+// compile-time relative-position-table column of key token `key`
+__host__ __device__ constexpr int key_tab(int key) { return (key / 7) * 13 + key % 7; }
+
 template <int WS, int HD>
-__global__ __launch_bounds__(256) void winattn_bwd_q_kernel(WinParams p, const float* __restrict__ biasT, int nitems) {
-  __shared__ float Ks[WA_WAVES][WA_NP][WA_HD];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void winattn_bwd_kernel(
+    WinParams p, const float* __restrict__ biasT, int nitems) {
+  __shared__ float tbuf[WA_WAVES][WA_NP][WA_TP];
   __shared__ float tabg[WA_WAVES][WA_T + 3];
+  __shared__ float padk[WA_WAVES][WA_HD], padv[WA_WAVES][WA_HD];
   __shared__ int8_t regs[WA_WAVES][WA_NP];
-  __shared__ int kidx[WA_NP];
+  __shared__ int rowtab[WA_WAVES][WA_NP];
   const WinGeom& g = p.g;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l31 = lane & 31, h = lane >> 5;
   const WaItem it = wa_item(p, nitems);
   const Win<WS> w(g, it.win);
   const int col0 = it.hh * HD;
-  for (int e = lane; e < WA_NP * HD / 4; e += 64) {
-    const int tok = e >> 3, c4 = e & 7;
-    const float4 v = tok < WA_N ? ld_tok4(p.k, p.qk_ld, w.row(g, tok), p.k_pad, col0 + 4 * c4)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(&Ks[wv][tok][4 * c4]) = v;
-  }
   for (int e = lane; e < WA_T + 3; e += 64) tabg[wv][e] = 0.f;
-  if (wv == 0) kidx[lane] = lane < WA_N ? (lane / WS) * (2 * WS - 1) + lane % WS : 0;
+  rowtab[wv][lane] = lane < WA_N ? w.row(g, lane) : -2;
+  if (lane < HD) { padk[wv][lane] = 0.f; padv[wv][lane] = 0.f; }
   const bool border = wa_regions(p, w, regs[wv], lane);
-  wa_f16x s[2][2], dp[2][2];
+
+  wa_f16x s[2][2], dp[2][2];  // S^T / P^T and dP^T / dS^T  [key tile][query tile]
   load_bias(s, biasT + (size_t)it.hh * 4096, lane);
-  float4 qf[2][4];
-  int qrow[2];
-  bool qreal[2];
+  int trow[2];
+  bool treal[2];
+  float D[2];
   {
-    float4 kf[2][4];
+    float4 kf[2][4], qf[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int tok = t * 32 + l31;
-      qreal[t] = tok < WA_N;
-      qrow[t] = qreal[t] ? w.row(g, tok) : -1;
-      load_frag(kf[t], p.k, p.qk_ld, qrow[t], p.k_pad, qreal[t], col0, h, 1.f);
-      load_frag(qf[t], p.q, p.qk_ld, qrow[t], p.q_pad, qreal[t], col0, h, p.scale);
+      treal[t] = tok < WA_N;
+      trow[t] = treal[t] ? w.row(g, tok) : -1;
+      load_frag(kf[t], p.k, p.qk_ld, trow[t], p.k_pad, treal[t], col0, h, 1.f);
+      load_frag(qf[t], p.q, p.qk_ld, trow[t], p.q_pad, treal[t], col0, h, p.scale);
     }
-    mma_hd(s, kf, qf);
+    mma_hd(s, kf, qf);  // S^T[key][q]
   }
-  float D[2];
   {
     float4 vf[2][4], df[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       // dO / O exist only for real (non-pad) query rows: pad and padding queries get 0
-      const bool qo = qreal[t] && qrow[t] >= 0;
-      load_frag(vf[t], p.v, p.v_ld, qrow[t], p.v_pad, qreal[t], col0, h, 1.f);
-      load_frag(df[t], p.dout, p.out_ld, qrow[t], nullptr, qo, col0, h, 1.f);
+      const bool qo = treal[t] && trow[t] >= 0;
+      load_frag(vf[t], p.v, p.v_ld, trow[t], p.v_pad, treal[t], col0, h, 1.f);
+      load_frag(df[t], p.dout, p.out_ld, trow[t], nullptr, qo, col0, h, 1.f);
       float4 of[4];
-      load_frag(of, p.out, p.out_ld, qrow[t], nullptr, qo, col0, h, 1.f);
+      load_frag(of, p.out, p.out_ld, trow[t], nullptr, qo, col0, h, 1.f);
       float part = 0.f;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) part += dot4(df[t][g4], of[g4]);
@@ -363,177 +392,132 @@ __global__ __launch_bounds__(256) void winattn_bwd_q_kernel(WinParams p, const f
         for (int r = 0; r < 16; ++r) dp[a][b][r] = 0.f;
     mma_hd(dp, vf, df);  // dP^T[key][q] = sum_d V[key][d] dO[q][d]
   }
-  __syncthreads();  // Ks, tabg, kidx, regs
-  float lse[2];
-  int bq[2];
-#pragma unroll
-  for (int n = 0; n < 2; ++n) {
-    const int q = n * 32 + l31;
-    lse[n] = (q < WA_N) ? p.lse[(int64_t)it.item * WA_N + q] : INFINITY;
-    bq[n] = q < WA_N ? (q / WS + WS - 1) * (2 * WS - 1) + q % WS + WS - 1 : -1;
-  }
-#pragma unroll
-  for (int n = 0; n < 2; ++n) {
-    const int rq = border ? regs[wv][n * 32 + l31] : 0;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = t * 32 + acc_row(r, h);
-        float sv = s[t][n][r];
-        if (border && regs[wv][key] != rq) sv -= 100.f;
-        const float ds = __expf(sv - lse[n]) * (dp[t][n][r] - D[n]);
-        dp[t][n][r] = ds;
-        if (bq[n] >= 0 && key < WA_N) atomicAdd(&tabg[wv][bq[n] - kidx[key]], ds);
-      }
-  }
-  wa_f16x dq[2];
-#pragma unroll
-  for (int n = 0; n < 2; ++n)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dq[n][r] = 0.f;
-  mma_tok(dq, Ks[wv], dp, l31, h);  // dQ^T[d][q] = sum_key K[key][d] dS^T[key][q]
-  if (it.active) {
+  wave_lds_sync();  // tabg, pads, regs
+  {
+    float lse[2];
+    int bq[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       const int q = n * 32 + l31;
-      if (q >= WA_N) continue;
-      if (h == 0) p.dsum[(int64_t)it.item * WA_N + q] = qrow[n] >= 0 ? D[n] : 0.f;
-      if (qrow[n] < 0) continue;
-      float* dst = p.dq + (int64_t)qrow[n] * p.dqk_ld + col0;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-        *reinterpret_cast<float4*>(dst + 8 * a + 4 * h) =
-            make_float4(dq[n][4 * a] * p.scale, dq[n][4 * a + 1] * p.scale, dq[n][4 * a + 2] * p.scale,
-                        dq[n][4 * a + 3] * p.scale);
-    }
-  }
-  __syncthreads();  // tabg complete
-  if (it.active) {
-    float* P = p.partial + (int64_t)it.item * (WA_T + 2 * HD);
-    for (int e = lane; e < WA_T; e += 64) P[e] = tabg[wv][e];
-  }
-}
-
-// Backward, key side (lane column = key): recompute P = exp(S - lse) with
-// S = Q K^T (rows = queries), dP = dO V^T, dS = P (dP - D);
-// dV^T = dO^T P, dK^T = (scale Q)^T dS.  Pad keys fold into per-item sums.
-template <int WS, int HD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void winattn_bwd_kv_kernel(WinParams p, const float* __restrict__ biasN, int nitems) {
-  __shared__ float Qs[WA_WAVES][WA_NP][WA_HD];  // scale * q
-  __shared__ float Ds[WA_WAVES][WA_NP][WA_HD];  // dO
-  __shared__ float lse_s[WA_WAVES][WA_NP], D_s[WA_WAVES][WA_NP];
-  __shared__ int8_t regs[WA_WAVES][WA_NP];
-  __shared__ float padk[WA_WAVES][WA_HD], padv[WA_WAVES][WA_HD];
-  const WinGeom& g = p.g;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l31 = lane & 31, h = lane >> 5;
-  const WaItem it = wa_item(p, nitems);
-  const Win<WS> w(g, it.win);
-  const int col0 = it.hh * HD;
-  for (int e = lane; e < WA_NP * HD / 4; e += 64) {
-    const int tok = e >> 3, c4 = e & 7;
-    const int row = tok < WA_N ? w.row(g, tok) : -1;
-    float4 qv = tok < WA_N ? ld_tok4(p.q, p.qk_ld, row, p.q_pad, col0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    qv.x *= p.scale; qv.y *= p.scale; qv.z *= p.scale; qv.w *= p.scale;
-    *reinterpret_cast<float4*>(&Qs[wv][tok][4 * c4]) = qv;
-    *reinterpret_cast<float4*>(&Ds[wv][tok][4 * c4]) =
-        row >= 0 ? *reinterpret_cast<const float4*>(p.dout + (int64_t)row * p.out_ld + col0 + 4 * c4)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  {
-    const bool qr = lane < WA_N;
-    lse_s[wv][lane] = qr ? p.lse[(int64_t)it.item * WA_N + lane] : INFINITY;  // +inf: P = 0
-    D_s[wv][lane] = qr ? p.dsum[(int64_t)it.item * WA_N + lane] : 0.f;
-  }
-  if (lane < HD) { padk[wv][lane] = 0.f; padv[wv][lane] = 0.f; }
-  const bool border = wa_regions(p, w, regs[wv], lane);
-  wa_f16x s[2][2], dp[2][2];  // [query tile][key tile]
-  load_bias(s, biasN + (size_t)it.hh * 4096, lane);
-  int krow[2];
-  bool kreal[2];
-  {
-    float4 qf[2][4], kf[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int tok = t * 32 + l31;
-      kreal[t] = tok < WA_N;
-      krow[t] = kreal[t] ? w.row(g, tok) : -1;
-      load_frag(qf[t], p.q, p.qk_ld, krow[t], p.q_pad, kreal[t], col0, h, p.scale);
-      load_frag(kf[t], p.k, p.qk_ld, krow[t], p.k_pad, kreal[t], col0, h, 1.f);
-    }
-    mma_hd(s, qf, kf);  // S[q][key]
-  }
-  {
-    float4 df[2][4], vf[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      load_frag(df[t], p.dout, p.out_ld, krow[t], nullptr, kreal[t] && krow[t] >= 0, col0, h, 1.f);
-      load_frag(vf[t], p.v, p.v_ld, krow[t], p.v_pad, kreal[t], col0, h, 1.f);
+      lse[n] = (q < WA_N) ? p.lse[(int64_t)it.item * WA_N + q] : INFINITY;  // +inf: P = 0
+      bq[n] = q < WA_N ? (q / WS + WS - 1) * (2 * WS - 1) + q % WS + WS - 1 : -1;
     }
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int n = 0; n < 2; ++n) {
+      const int rq = border ? regs[wv][n * 32 + l31] : 0;
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dp[a][b][r] = 0.f;
-    mma_hd(dp, df, vf);  // dP[q][key]
+        for (int r = 0; r < 16; ++r) {
+          const int key0 = t * 32 + acc_row(r, 0);  // key of lane half 0; half 1: key0 + 4
+          const int key = key0 + 4 * h;
+          float sv = s[t][n][r];
+          if (border && regs[wv][key] != rq) sv -= 100.f;
+          const float pr = __expf(sv - lse[n]);
+          const float ds = pr * (dp[t][n][r] - D[n]);
+          s[t][n][r] = pr;
+          dp[t][n][r] = ds;
+          const bool kin = h ? (key0 + 4 < WA_N) : (key0 < WA_N);
+          const int kt = h ? key_tab(key0 + 4) : key_tab(key0);
+          if (bq[n] >= 0 && kin) atomicAdd(&tabg[wv][bq[n] - kt], ds);
+        }
+    }
   }
-  __syncthreads();  // Qs, Ds, lse_s, D_s, regs, pads
+  // ---- products over the score tiles, each read back from the per-wave LDS image ----
+  auto to_lds = [&](const wa_f16x (&x)[2][2]) {
 #pragma unroll
-  for (int n = 0; n < 2; ++n) {
-    const int rk = border ? regs[wv][n * 32 + l31] : 0;
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tbuf[wv][t * 32 + acc_row(r, h)][n * 32 + l31] = x[t][n][r];
+  };
+  // acc[ti][r] = sum_q tbuf[ti*32 + l31][q] * col[q], q = 2j + h; row key = ti*32 + acc_row(r, h), column d = l31
+  auto key_side = [&](const float (&colv)[25], float* gbase, int64_t gld, float* padacc) {
+    wa_f16x acc[2];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ti][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 25; ++j)
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) acc[ti] = mfma32(tbuf[wv][ti * 32 + l31][2 * j + h], colv[j], acc[ti]);
+    if (!it.active) return;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rowtab[wv][ti * 32 + acc_row(r, h)];
+        if (row >= 0) gbase[(int64_t)row * gld + col0 + l31] = acc[ti][r];
+        else if (row == -1) atomicAdd(&padacc[l31], acc[ti][r]);  // pad key: into the Linear-bias gradient
+      }
+  };
+  // dV[key][d] = sum_q P^T[key][q] dO[q][d]
+  {
+    float dc[25];
+#pragma unroll
+    for (int j = 0; j < 25; ++j) {
+      dc[j] = col_val(p.dout, p.out_ld, nullptr, rowtab[wv][2 * j + h], col0 + l31);
+    }
+    to_lds(s);
+    wave_lds_sync();
+    key_side(dc, p.dv, p.dv_ld, padv[wv]);
+  }
+  wave_lds_sync();  // every P^T read done
+  to_lds(dp);
+  wave_lds_sync();
+  // dQ^T[d][q] = sum_key K[key][d] dS^T[key][q]  (K columns from global, dS^T from LDS)
+  {
+    float kc[2][16];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int q = t * 32 + acc_row(r, h);
-        float sv = s[t][n][r];
-        if (border && regs[wv][q] != rk) sv -= 100.f;
-        const float pr = __expf(sv - lse_s[wv][q]);
-        s[t][n][r] = pr;
-        dp[t][n][r] = pr * (dp[t][n][r] - D_s[wv][q]);
+        kc[t][r] = col_val(p.k, p.qk_ld, p.k_pad, rowtab[wv][t * 32 + acc_row(r, h)], col0 + l31);
       }
-  }
-  // dV first, then dK: P dies before the dK accumulators go live
-  auto store_grad = [&](const wa_f16x (&gacc)[2], float* gbase, int64_t gld, float* padacc) {
+    wa_f16x dq[2];
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      if (!it.active || !kreal[n]) continue;
-      if (krow[n] >= 0) {
-        float* dst = gbase + (int64_t)krow[n] * gld + col0;
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[n][r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < (t == 0 ? 16 : 12); ++r)  // keys >= 56: all padding
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          dq[n] = mfma32(kc[t][r], tbuf[wv][t * 32 + acc_row(r, h)][n * 32 + l31], dq[n]);
+    if (it.active) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        if (!treal[n] || trow[n] < 0) continue;  // padding / pad query: cropped away
+        float* dst = p.dq + (int64_t)trow[n] * p.dqk_ld + col0;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
           *reinterpret_cast<float4*>(dst + 8 * a + 4 * h) =
-              make_float4(gacc[n][4 * a], gacc[n][4 * a + 1], gacc[n][4 * a + 2], gacc[n][4 * a + 3]);
-      } else {  // pad key: its k / v were the Linear bias (or 0) -> sum into the bias gradient
-#pragma unroll
-        for (int r = 0; r < 16; ++r) atomicAdd(&padacc[acc_row(r, h)], gacc[n][r]);
+              make_float4(dq[n][4 * a] * p.scale, dq[n][4 * a + 1] * p.scale, dq[n][4 * a + 2] * p.scale,
+                          dq[n][4 * a + 3] * p.scale);
       }
     }
-  };
-  {
-    wa_f16x dv[2];
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dv[n][r] = 0.f;
-    mma_tok(dv, Ds[wv], s, l31, h);  // dV^T[d][key] = sum_q dO[q][d] P[q][key]
-    store_grad(dv, p.dv, p.dv_ld, padv[wv]);
   }
+  // dK[key][d] = sum_q dS^T[key][q] (scale Q)[q][d]
   {
-    wa_f16x dk[2];
+    float qc[25];
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dk[n][r] = 0.f;
-    mma_tok(dk, Qs[wv], dp, l31, h);  // dK^T[d][key] = sum_q (scale q)[q][d] dS[q][key]
-    store_grad(dk, p.dk, p.dqk_ld, padk[wv]);
+    for (int j = 0; j < 25; ++j) {
+      qc[j] = p.scale * col_val(p.q, p.qk_ld, p.q_pad, rowtab[wv][2 * j + h], col0 + l31);
+    }
+    key_side(qc, p.dk, p.dqk_ld, padk[wv]);
   }
-  __syncthreads();
-  if (it.active && lane < HD) {
+  wave_lds_sync();  // tabg, pads complete
+  if (it.active) {
     float* P = p.partial + (int64_t)it.item * (WA_T + 2 * HD);
-    P[WA_T + lane] = padk[wv][lane];
-    P[WA_T + HD + lane] = padv[wv][lane];
+    for (int e = lane; e < WA_T; e += 64) P[e] = tabg[wv][e];
+    if (lane < HD) {
+      P[WA_T + lane] = padk[wv][lane];
+      P[WA_T + HD + lane] = padv[wv][lane];
+    }
   }
 }
 
@@ -633,17 +617,16 @@ extern "C" int mdemi_winattn_fwd(const mdemi_winattn_desc* d, void* stream) {
   return check_launch("winattn_fwd");
 }
 
-// workspace: [partials items x R | D items x N | bias T | bias N | sums heads*R | colsum scratch]
+// workspace: [partials items x R | bias T | sums heads*R | colsum scratch]
 static size_t wa_part_bytes(int items, int R) { return align_up((size_t)items * R * 4, 256); }
-static size_t wa_dsum_bytes(int items) { return align_up((size_t)items * WA_N * 4, 256); }
 extern "C" size_t mdemi_winattn_bwd_workspace_size(const mdemi_winattn_desc* d) {
   WinParams p;
   int nwin;
   if (make_params(d, p, nwin)) return 0;
   const int R = WA_T + 2 * WA_HD;
   const int items = wa_items(d, nwin);
-  return wa_part_bytes(items, R) + wa_dsum_bytes(items) + 2 * wa_bias_bytes(d) +
-         align_up((size_t)d->heads * R * 4, 256) + colsum_ws_bytes(nwin, (int64_t)d->heads * R);
+  return wa_part_bytes(items, R) + wa_bias_bytes(d) + align_up((size_t)d->heads * R * 4, 256) +
+         colsum_ws_bytes(nwin, (int64_t)d->heads * R);
 }
 
 extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
@@ -664,15 +647,13 @@ extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
   const int items = wa_items(d, nwin);
   char* ws = (char*)d->workspace;
   p.partial = (float*)ws;
-  p.dsum = (float*)(ws + wa_part_bytes(items, R));
-  float* biasT = (float*)((char*)p.dsum + wa_dsum_bytes(items));
-  float* biasN = (float*)((char*)biasT + wa_bias_bytes(d));
-  float* sums = (float*)((char*)biasN + wa_bias_bytes(d));
+  float* biasT = (float*)(ws + wa_part_bytes(items, R));
+  float* sums = (float*)((char*)biasT + wa_bias_bytes(d));
   void* cws = (char*)sums + align_up((size_t)d->heads * R * 4, 256);
-  hipLaunchKernelGGL(wa_bias_kernel, dim3(d->heads * 16), dim3(256), 0, st, d->rpb_table, d->heads, biasT, biasN);
-  const dim3 grid((unsigned)cdiv(items, WA_WAVES)), block(64 * WA_WAVES);
-  hipLaunchKernelGGL((winattn_bwd_q_kernel<7, 32>), grid, block, 0, st, p, (const float*)biasT, items);
-  hipLaunchKernelGGL((winattn_bwd_kv_kernel<7, 32>), grid, block, 0, st, p, (const float*)biasN, items);
+  hipLaunchKernelGGL(wa_bias_kernel, dim3(d->heads * 16), dim3(256), 0, st, d->rpb_table, d->heads, biasT,
+                     (float*)nullptr);
+  hipLaunchKernelGGL((winattn_bwd_kernel<7, 32>), dim3((unsigned)cdiv(items, WA_WAVES)), dim3(64 * WA_WAVES), 0, st,
+                     p, (const float*)biasT, items);
   int rc2 = colsum_launch(p.partial, nwin, (int64_t)d->heads * R, (int64_t)d->heads * R, sums, 0, cws, st);
   if (rc2) return rc2;
   hipLaunchKernelGGL((winattn_bwd_scatter<7, 32>), dim3((d->heads * R + 255) / 256), dim3(256), 0, st, sums, d->heads,
