@@ -38,6 +38,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (v_mfma_f32_32x32x2_f32)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense BF16 MFMA (no sparsity)
 HBM_PEAK_GBS = 8000.0
 CPU_SHARE_PER_GPU = 16  # the GPU box's host-CPU share per GPU (OMP_NUM_THREADS there)
 
@@ -84,6 +85,11 @@ WORKLOADS = {
     "depthformer": dict(opt=_DFV8_NYU, model="DepthformerV8-B5", h=480, w=640,
                         workload="Depthformer v8 train step, NYU 480x640 (fp32)",
                         ref_cfg="json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json"),
+    # BASELINE configs[4]: bf16 mixed precision (bf16 GEMM operands, fp32 accumulate / master
+    # weights / optimizer) with the whole train step captured in one hipGraph
+    "depthformer_bf16": dict(opt=_DFV8_NYU, model="DepthformerV8-B5", h=480, w=640, precision="bf16", graph=True,
+                             workload="Depthformer v8 train step, NYU 480x640, bf16 mixed precision, hipGraph",
+                             ref_cfg="json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json"),
 }
 # HBM bytes per launch of the roofline kernel family, from the committed
 # rocprofv3 --pmc passes (tools/pmc_traffic.py; FETCH_SIZE doubled per the
@@ -106,6 +112,9 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the KITTI 352x1216 secondary line")
+    ap.add_argument("--precision", default=None, choices=["fp32", "bf16"],
+                    help="matmul precision (default: the workload's; bf16 = bf16 operands, fp32 accumulate)")
+    ap.add_argument("--graph", action="store_true", help="capture the whole train step in a hipGraph")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: launcher/gloo plumbing check only (a toy model, not a measurement)")
     return ap.parse_args()
@@ -175,8 +184,9 @@ def _gemm_alg_bytes(A, B, M, N, K, kw):
 
 
 def gemm_roofline(trainer, batches):
-    """One instrumented step: HIP events around every libmdemi GEMM launch on its stream;
-    algorithmic FLOPs (2*M*N*K per GEMM) and bytes / measured kernel time, per kernel family."""
+    """One instrumented (eager, even for a captured trainer) step: HIP events around every
+    libmdemi GEMM launch on its stream; algorithmic FLOPs (2*M*N*K per GEMM) and bytes /
+    measured kernel time, per kernel family."""
     from mdemi import functional as mf
     recs = []
     orig = mf.gemm
@@ -192,7 +202,8 @@ def gemm_roofline(trainer, batches):
 
     mf.gemm = timed
     try:
-        trainer.step(batches)
+        with mf.matmul_precision(trainer.precision):
+            trainer._eager_step(batches)
         torch.cuda.synchronize()
     finally:
         mf.gemm = orig
@@ -224,15 +235,18 @@ def roofline_entry(trainer, batches, workload_key, ms):
     by, dom, tot_fl, tot_t = gemm_roofline(trainer, batches)
     (al, bl, aop, bop), (fl, t, cnt, alg) = dom
     ach = fl / t / 1e12
-    regex = f"gemm_f32_kernel<{al}, {bl}, {aop}, {bop},"
+    bf16 = trainer.precision == "bf16"
+    kname = "gemm_bf16_kernel" if bf16 else "gemm_f32_kernel"
+    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
+    regex = f"{kname}<{al}, {bl}, {aop}, {bop},"
     traffic = profiled_traffic(regex, workload_key)
     alg_pl = alg / cnt
-    roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+    roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4),
             "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
             "algorithmic_bytes": round(alg_pl), "traffic_over_algorithmic":
                 (round(traffic / alg_pl, 3) if traffic else None),
-            "kernel": f"gemm_f32_kernel<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}> (all pipelining variants)",
+            "kernel": f"{kname}<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}> (all pipelining variants)",
             "kernel_regex": regex, "launches": cnt, "avg_launch_us": round(t / cnt * 1e6, 2),
             "flops_per_launch": fl / cnt}
     fams = {f"{KERNEL_NAME[k[0]]},{KERNEL_NAME[k[1]]},{k[2]},{k[3]}": {
@@ -240,8 +254,8 @@ def roofline_entry(trainer, batches, workload_key, ms):
         "algorithmic_GBps": round(v[3] / v[1] / 1e9, 1)} for k, v in sorted(by.items(), key=lambda kv: -kv[1][1])}
     extra = {"gemm_all": {"achieved_tflops": round(tot_fl / tot_t / 1e12, 2), "gemm_ms_per_step": round(tot_t * 1e3, 2),
                           "gemm_tflop_per_step": round(tot_fl / 1e12, 3),
-                          "frac": round(tot_fl / tot_t / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4), "families": fams},
-             "step_mfma_frac": round(tot_fl / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
+                          "frac": round(tot_fl / tot_t / 1e12 / peak, 4), "families": fams},
+             "step_mfma_frac": round(tot_fl / (ms * 1e-3) / 1e12 / peak, 4)}
     return roof, extra
 
 
@@ -315,13 +329,13 @@ def cpu_baseline(model, opt, H, W, budget_s):
 
 
 # --------------------------------------------------------------------------- one measurement
-def measure(args, opt, key, H, W, B, rank, world, device, with_roofline):
+def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precision="fp32", graph=False):
     """Build the trainer from `opt`, run W warm-up + K timed steps; returns a dict."""
     from mdemi.train import build_from_config
     opt = copy.deepcopy(opt)
     opt["dataloader"]["batch_size"] = B
     torch.manual_seed(0)
-    trainer = build_from_config(opt, device=device, world=world)
+    trainer = build_from_config(opt, device=device, world=world, precision=precision, graph=graph)
     na = trainer.num_accum
     batches = [synthetic_batch(B, H, W, device, seed=1000 + 7 * rank + i, data_type=opt["dataset"]["data_type"])
                for i in range(na)]
@@ -459,8 +473,14 @@ def main():
         opt, ref_cfg = wl["opt"], wl["ref_cfg"]
         H, W = args.height or wl["h"], args.width or wl["w"]
     B = args.batch or int(opt["dataloader"]["batch_size"])
+    precision = args.precision or wl.get("precision", "fp32")
+    graph = args.graph or wl.get("graph", False)
+    if graph and world > 1:
+        print("bench: the hipGraph-captured step is single-GPU in this build; running eagerly", file=sys.stderr)
+        graph = False
 
-    res = measure(args, opt, key, H, W, B, rank, world, device, with_roofline=not args.no_roofline)
+    res = measure(args, opt, key, H, W, B, rank, world, device, with_roofline=not args.no_roofline,
+                  precision=precision, graph=graph)
     value = res["images"] / res["elapsed"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -492,10 +512,12 @@ def main():
                        f"images/sec (train step) {wl['model']} {W}x{H} bs={B}/GPU"),
             "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(res["ms"], 2), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights)",
+            "vs_baseline": None, "dtype": "bf16" if precision == "bf16" else "fp32",
+            "data": "synthetic (random-init weights)",
             "config": {"workload": wl["workload"], "model": wl["model"], "global_batch": B * world,
                        "per_gpu_batch": B, "num_accum": res["num_accum"], "image": [H, W],
-                       "parallelism": f"dp{world}", "reference_config": ref_cfg},
+                       "parallelism": f"dp{world}", "reference_config": ref_cfg,
+                       "matmul_precision": precision, "hipgraph": graph},
             "roofline": res.get("roofline"), "cpu_baseline": cpu, "loss": round(res["loss"], 5),
             "rccl_world": world if world > 1 else None,
         }

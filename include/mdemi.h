@@ -113,6 +113,14 @@ typedef struct mdemi_gemm_desc {
 
 size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d);
 int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream);
+/* Same contract with bf16 compute (mixed precision, BASELINE configs[4] "bf16"
+ * = torch.autocast's matmul numerics): fp32 operands are rounded to bf16 (RNE)
+ * as they are staged, products run on the bf16 MFMA with fp32 accumulation,
+ * and the fp32 epilogue and output are those of mdemi_gemm_f32.  Replaces the
+ * autocast bf16 addmm/bmm/conv of the reference's layers (e.g.
+ * model/Depthformer/luna_layer.py:181-259, layer_utils.py:6-34) for the
+ * mixed-precision train step.  Workspace: mdemi_gemm_workspace_size. */
+int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream);
 /* tuning hook: pipelining variant (0..5, see gemm_f32.hip; -1 = time the
  * candidates once per distinct shape and cache the winner, the default -- all
  * variants produce bit-identical results) and tile raster (group_m > 0:
@@ -350,6 +358,17 @@ int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                      const mdemi_adamw_group* groups_host, int32_t ngroups,
                      const float* sumsq, float max_norm, int32_t step, int64_t nitems,
                      void* workspace, void* stream);
+/* Capturable form (a hipGraph-captured train step): the hyperparameters come
+ * from device memory.  sched_dev is a [nsteps][ngroups] table of
+ * mdemi_adamw_group entries -- e.g. the OneCycle lr / beta1 of every optimizer step --
+ * *step_dev the number of steps already taken: the update uses row
+ * min(*step_dev, nsteps - 1) and bias corrections for step *step_dev + 1, then a
+ * trailing one-thread kernel increments *step_dev.  Same numerics as
+ * mdemi_adamw_step. */
+int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
+                         const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
+                         int32_t* step_dev, const float* sumsq, float max_norm, int64_t nitems,
+                         void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

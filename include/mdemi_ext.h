@@ -82,6 +82,11 @@ int mdemi_act_fwd(const float* x, float* y, int64_t n, int32_t act, void* stream
  * same call on dy (nn.Dropout in layers.py:8, luna_layer.py:172-173,
  * feed_forward.py:26, decoder_v8.py:84,87).  p == 0 is a copy. */
 int mdemi_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, uint64_t offset, void* stream);
+/* mdemi_dropout with the seed read from device memory (seed_dev[0] + seed_add):
+ * the caller draws seed_dev on the GPU (torch's graph-safe Philox), so a
+ * hipGraph-captured train step gets a fresh mask on every replay. */
+int mdemi_dropout_dev(const float* x, float* y, int64_t n, float p, const uint64_t* seed_dev, uint64_t seed_add,
+                      uint64_t offset, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Channels-last adaptive-bin head: logits [B][HW][K] (the 1x1 conv_out /    */

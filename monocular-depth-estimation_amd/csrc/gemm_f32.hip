@@ -341,6 +341,7 @@ __device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles
   tn = in_grp / gm;
 }
 
+
 // Pipelining variants (A/B-tested on the model's shapes, tools/gemm_bench.py):
 //   BK    K depth per LDS tile (16 or 32)
 //   NBUF  LDS buffers (2: write the next tile while others read this one)
@@ -473,101 +474,158 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
     }
   }
 
-  // Epilogue.  acc[im][in][r] holds C(row, col) with
-  //   row = bm + wm*64 + im*32 + (r&3) + 8*(r>>2) + 4*h,  col = bn + wn*64 + in*32 + l31
-  // Every operand is addressed through a buffer descriptor at the tile origin
-  // with 32-bit offsets; out-of-tile elements get BUF_OOB (loads read 0,
-  // stores are dropped), so the fused stages below are straight-line code
-  // with wave-uniform stage selection.
-  int colb[2];
-  bool colok[2];
+#include "gemm_epilogue.inc"
+}
+
+// ---------------------------------------------------------------------------
+// bf16-compute variant (mixed precision, BASELINE configs[4]): the same
+// operand loaders fetch fp32 from HBM, values are rounded to bf16 (RNE,
+// v_cvt_pk_bf16_f32) on their way into LDS, products run on
+// v_mfma_f32_32x32x16_bf16 (16x the fp32 MFMA rate) with fp32 accumulation,
+// and the fp32 epilogue is shared with the fp32 kernel.  This is autocast's
+// numerics (bf16 operands, fp32 accumulate) with an fp32 result.
+//
+// LDS images are [row][k] bf16 for both operands (B as [col][k]), pitch
+// BK + 8 elements: a lane's MFMA fragment (8 consecutive k of one row) is one
+// conflict-free ds_read_b128.  k-contiguous sources (row-major A, [N][K]
+// weights, NHWC im2col rows) store 4 bf16 per float4 with one ds_write_b64;
+// m/n-contiguous sources scatter 4 ds_write_b16 per float4.
+// MFMA 32x32x16 lane maps: lane l (r = l&31, h = l>>5) holds A[r][8h + j] and
+// B[8h + j][r], j = 0..7, for the 16-deep k-step.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+template <int IMG, int BK>
+__device__ __forceinline__ void store_bf16(__bf16* img, int t, const float4 (&r)[BK / 8]) {
+  constexpr int PB = BK + 8, NQ = BK / 8;
+  if constexpr (IMG == IMG_KR) {  // float4 runs along rows/cols at one k: k = t/32 + 8q, cols 4*(t&31) + i
 #pragma unroll
-  for (int in = 0; in < 2; ++in) {
-    const int jl = wn * 64 + in * 32 + l31;
-    colok[in] = bn + jl < p.N;
-    colb[in] = jl;
-  }
-  auto rowl = [&](int im, int r) { return wm * 64 + im * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
-  auto off = [&](int64_t ld, int im, int in, int r) {
-    const int il = rowl(im, r);
-    return (colok[in] && bm + il < p.M) ? (int)((il * ld + colb[in]) * 4) : BUF_OOB;
-  };
-#define MDEMI_EACH for (int r = 0; r < 16; ++r)
-  if (p.split > 1) {
-    const auto rs = make_rsrc(p.slab + (((int64_t)sidx * p.batch + b) * p.M + bm) * p.N + bn);
-#pragma unroll
-    for (int im = 0; im < 2; ++im)
-#pragma unroll
-      for (int in = 0; in < 2; ++in)
-#pragma unroll
-        MDEMI_EACH __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[im][in][r]), rs, off(p.N, im, in, r), 0, 0);
-    return;
-  }
-  const int64_t cbase = (int64_t)b * p.c_bs + (int64_t)bm * p.ldc + bn;
-  const auto rc = make_rsrc(p.C + cbase);
-  // one 32x32 accumulator at a time keeps the epilogue's live offsets to 16
-#pragma unroll
-  for (int im = 0; im < 2; ++im)
-#pragma unroll
-    for (int in = 0; in < 2; ++in) {
-      floatx16& v = acc[im][in];
-      if (p.alpha != 1.f) {
-#pragma unroll
-        MDEMI_EACH v[r] *= p.alpha;
-      }
-      if (p.beta != 0.f) {
-#pragma unroll
-        MDEMI_EACH v[r] = fmaf(p.beta, buf_ld1(rc, off(p.ldc, im, in, r)), v[r]);
-      }
-      if (p.bias_mode == MDEMI_BIAS_COL) {
-        const float bj = colok[in] ? p.bias[bn + colb[in]] : 0.f;
-#pragma unroll
-        MDEMI_EACH v[r] += bj;
-      } else if (p.bias_mode == MDEMI_BIAS_ROW) {
-        const auto rs = make_rsrc(p.bias + bm);
-#pragma unroll
-        MDEMI_EACH v[r] += buf_ld1(rs, bm + rowl(im, r) < p.M ? rowl(im, r) * 4 : BUF_OOB);
-      }
-      if (p.pre) {
-        const auto rs = make_rsrc(p.pre + (int64_t)b * p.pre_bs + (int64_t)bm * p.ldpre + bn);
-#pragma unroll
-        MDEMI_EACH __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rs, off(p.ldpre, im, in, r), 0, 0);
-      }
-      switch (p.act) {
-        case MDEMI_ACT_GELU: {
-#pragma unroll
-          MDEMI_EACH v[r] = gelu_f(v[r]);
-        } break;
-        case MDEMI_ACT_RELU: {
-#pragma unroll
-          MDEMI_EACH v[r] = fmaxf(v[r], 0.f);
-        } break;
-        case MDEMI_ACT_GELU_GRAD: {
-          const auto rs = make_rsrc(p.aux + (int64_t)b * p.aux_bs + (int64_t)bm * p.ldaux + bn);
-#pragma unroll
-          MDEMI_EACH v[r] *= gelu_grad_f(buf_ld1(rs, off(p.ldaux, im, in, r)));
-        } break;
-        case MDEMI_ACT_RELU_GRAD:
-        case MDEMI_ACT_SILU_GRAD: {
-          const auto rs = make_rsrc(p.aux + (int64_t)b * p.aux_bs + (int64_t)bm * p.ldaux + bn);
-#pragma unroll
-          MDEMI_EACH v[r] *= aux_grad(p.act, buf_ld1(rs, off(p.ldaux, im, in, r)));
-        } break;
-        case MDEMI_ACT_NONE: break;
-        default: {
-#pragma unroll
-          MDEMI_EACH v[r] = apply_act(p.act, v[r]);
-        }
-      }
-      if (p.res) {
-        const auto rs = make_rsrc(p.res + (int64_t)b * p.res_bs + (int64_t)bm * p.ldres + bn);
-#pragma unroll
-        MDEMI_EACH v[r] += buf_ld1(rs, off(p.ldres, im, in, r));
-      }
-#pragma unroll
-      MDEMI_EACH __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rc, off(p.ldc, im, in, r), 0, 0);
+    for (int q = 0; q < NQ; ++q) {
+      __bf16* d = img + (4 * (t & 31)) * PB + (t >> 5) + 8 * q;
+      d[0] = (__bf16)r[q].x;
+      d[PB] = (__bf16)r[q].y;
+      d[2 * PB] = (__bf16)r[q].z;
+      d[3 * PB] = (__bf16)r[q].w;
     }
-#undef MDEMI_EACH
+  } else {  // float4 runs along k: row t/KQ + RS*q, k 4*(t%KQ)
+    constexpr int KQ = BK / 4, RS = 256 / KQ;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      bf16x4_t v;
+      v[0] = (__bf16)r[q].x; v[1] = (__bf16)r[q].y; v[2] = (__bf16)r[q].z; v[3] = (__bf16)r[q].w;
+      *reinterpret_cast<bf16x4_t*>(img + (t / KQ + RS * q) * PB + 4 * (t % KQ)) = v;
+    }
+  }
+}
+
+template <int AL, int BL, int AOP, int BOP, int BK, int OCC>
+__global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void gemm_bf16_kernel(GemmParams p) {
+  using LA = Loader<AL, AOP, true, BK, false>;
+  using LB = Loader<BL, BOP, false, BK, false>;
+  constexpr int NQ = BK / 8, PB = BK + 8, IMGE = GBM * PB;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * IMGE];
+
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int zb = blockIdx.x / ntiles;
+  int tm, tn;
+  tile_of(p, blockIdx.x % ntiles, ntiles, tm, tn);
+  const int b = zb / p.split, sidx = zb % p.split;
+  const int bm = tm * GBM, bn = tn * GBN;
+
+  LA la;
+  LB lb;
+  la.init(p.A + (int64_t)b * p.a_bs, p.lda, p.M, p.K, p.a_vec, bm, t, p);
+  lb.init(p.B + (int64_t)b * p.b_bs, p.ldb, p.N, p.K, p.b_vec, bn, t, p);
+
+  const int ktiles_total = (p.K + BK - 1) / BK;
+  const int kt_begin = sidx * p.ktile_per_split;
+  const int kt_end = min(ktiles_total, kt_begin + p.ktile_per_split);
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+
+  float4 ra[NQ], rb[NQ];
+  constexpr bool CAN_RSUM = AL == MDEMI_L_MNCONTIG;
+  const bool do_rsum = CAN_RSUM && p.rowsum != nullptr && tn == 0;
+  float4 rsum = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto acc_rsum = [&]() {  // fp32 row sums of the unrounded A (bias gradient)
+    if (CAN_RSUM && do_rsum) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        rsum.x += ra[q].x; rsum.y += ra[q].y; rsum.z += ra[q].z; rsum.w += ra[q].w;
+      }
+    }
+  };
+  const int l31 = lane & 31, h = lane >> 5;
+  const int ra0 = wm * 64 + l31, ra1 = ra0 + 32;
+  const int rb0 = wn * 64 + l31, rb1 = rb0 + 32;
+
+  if (kt_begin < kt_end) {
+    la.load(kt_begin * BK, ra);
+    lb.load(kt_begin * BK, rb);
+    store_bf16<LA::IMG, BK>(smem, t, ra);
+    store_bf16<LB::IMG, BK>(smem + IMGE, t, rb);
+    acc_rsum();
+    __syncthreads();
+  }
+  int cur = 0;
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const bool more = kt + 1 < kt_end;
+    if (more) {  // issue the next tile's loads early; they land under the MFMAs
+      la.load((kt + 1) * BK, ra);
+      lb.load((kt + 1) * BK, rb);
+    }
+    const __bf16* a_s = smem + cur * 2 * IMGE;
+    const __bf16* b_s = a_s + IMGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int ko = 16 * kk + 8 * h;
+      const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(a_s + ra0 * PB + ko);
+      const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(a_s + ra1 * PB + ko);
+      const bf16x8_t b0 = *reinterpret_cast<const bf16x8_t*>(b_s + rb0 * PB + ko);
+      const bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(b_s + rb1 * PB + ko);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      __bf16* dst = smem + (cur ^ 1) * 2 * IMGE;
+      store_bf16<LA::IMG, BK>(dst, t, ra);
+      store_bf16<LB::IMG, BK>(dst + IMGE, t, rb);
+      acc_rsum();
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (CAN_RSUM && do_rsum) {  // reduce the 8 k-row groups (t >> 5) through LDS
+    float4* red = reinterpret_cast<float4*>(smem);
+    red[t] = rsum;
+    __syncthreads();
+    if (t < 32) {
+      float4 s4 = red[t];
+#pragma unroll
+      for (int g = 1; g < 8; ++g) {
+        const float4 o = red[t + 32 * g];
+        s4.x += o.x; s4.y += o.y; s4.z += o.z; s4.w += o.w;
+      }
+      float* dst = p.rowsum + (p.split > 1 ? (int64_t)sidx * p.M : 0);
+      const int i = bm + 4 * t;
+      if (i + 0 < p.M) dst[i + 0] = s4.x;
+      if (i + 1 < p.M) dst[i + 1] = s4.y;
+      if (i + 2 < p.M) dst[i + 2] = s4.z;
+      if (i + 3 < p.M) dst[i + 3] = s4.w;
+    }
+  }
+#include "gemm_epilogue.inc"
 }
 
 // Deterministic split-K combine + epilogue: sums slabs in split order.
@@ -630,6 +688,7 @@ using KernelFn = void (*)(GemmParams);
 // boundaries, so the choice never changes a result bit.
 constexpr int NVARIANTS = 6;
 static int g_variant = -1;  // -1: autotune per shape
+static int g_variant_bf16 = -1;
 static int g_group_m = 8;
 
 template <int AL, int BL, int AOP, int BOP>
@@ -671,7 +730,39 @@ static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
   return nullptr;
 }
 
-static int variant_bk(int v) { return v >= 3 ? 32 : 16; }
+// bf16-compute family: variant 0 = BK 32 (2 workgroups/CU by LDS), 1 = BK 64.
+template <int AL, int BL, int AOP, int BOP>
+static KernelFn pick_variant_bf16(int v) {
+  if (v == 1) return gemm_bf16_kernel<AL, BL, AOP, BOP, 64, 1>;
+  return gemm_bf16_kernel<AL, BL, AOP, BOP, 32, 2>;
+}
+template <int AL, int BL>
+static KernelFn pick_ops_bf16(int aop, int bop, int v) {
+  if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_NONE) return pick_variant_bf16<AL, BL, MDEMI_OP_NONE, MDEMI_OP_NONE>(v);
+  if constexpr (AL == MDEMI_L_KCONTIG)
+    if (aop == MDEMI_OP_GELU && bop == MDEMI_OP_NONE)
+      return pick_variant_bf16<AL, BL, MDEMI_OP_GELU, MDEMI_OP_NONE>(v);
+  if constexpr (BL == MDEMI_L_MNCONTIG)
+    if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_GELU)
+      return pick_variant_bf16<AL, BL, MDEMI_OP_NONE, MDEMI_OP_GELU>(v);
+  return nullptr;
+}
+static KernelFn pick_kernel_bf16(int al, int bl, int aop, int bop, int v) {
+#define MDEMI_PICK(X, Y) \
+  if (al == X && bl == Y) return pick_ops_bf16<X, Y>(aop, bop, v);
+  MDEMI_PICK(MDEMI_L_KCONTIG, MDEMI_L_KCONTIG)
+  MDEMI_PICK(MDEMI_L_KCONTIG, MDEMI_L_MNCONTIG)
+  MDEMI_PICK(MDEMI_L_MNCONTIG, MDEMI_L_KCONTIG)
+  MDEMI_PICK(MDEMI_L_MNCONTIG, MDEMI_L_MNCONTIG)
+  MDEMI_PICK(MDEMI_L_CONV, MDEMI_L_KCONTIG)
+  MDEMI_PICK(MDEMI_L_CONV, MDEMI_L_MNCONTIG)
+  MDEMI_PICK(MDEMI_L_MNCONTIG, MDEMI_L_CONV)
+  MDEMI_PICK(MDEMI_L_KCONTIG, MDEMI_L_CONV)
+#undef MDEMI_PICK
+  return nullptr;
+}
+
+static int variant_bk(int v, bool bf16) { return bf16 ? (v == 1 ? 64 : 32) : (v >= 3 ? 32 : 16); }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -710,8 +801,8 @@ static int validate(const mdemi_gemm_desc* d) {
   return MDEMI_OK;
 }
 
-static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant) {
-  const int GBK = variant_bk(variant);
+static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, bool bf16) {
+  const int GBK = variant_bk(variant, bf16);
   p.M = d->M; p.N = d->N; p.K = d->K; p.batch = d->batch;
   p.A = d->A; p.lda = d->lda; p.a_bs = d->a_bstride;
   p.B = d->B; p.ldb = d->ldb; p.b_bs = d->b_bstride;
@@ -723,11 +814,13 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant) {
   p.cv = d->conv;
   p.pre = d->preact; p.ldpre = d->ldpre; p.pre_bs = d->pre_bstride;
   p.rowsum = d->rowsum_a;
-  // split boundaries in 32-element K chunks whatever the variant's BK
-  const int kc = (int)cdiv(d->K, 32);
+  // split boundaries in fixed K chunks whatever the variant's BK (32 elements for the
+  // fp32 family, 64 for bf16), so the variants of a family agree bit for bit
+  const int CH = bf16 ? 64 : 32;
+  const int kc = (int)cdiv(d->K, CH);
   const int split = d->split_k < kc ? d->split_k : kc;
   const int chunks_per_split = (int)cdiv(kc, split);
-  p.ktile_per_split = chunks_per_split * (32 / GBK);
+  p.ktile_per_split = chunks_per_split * (CH / GBK);
   p.split = (int)cdiv(kc, chunks_per_split);
   // vector loads need every row start 16-B aligned and whole quads in range
   // (KCONTIG: K % 4; MNCONTIG: the row/column extent % 4)
@@ -766,15 +859,16 @@ static size_t colsum_combine_bytes(const mdemi_gemm_desc* d, const GemmParams& p
   return colsum_combine(d, p) ? colsum_ws_bytes(p.split, (int64_t)d->M * d->N) : 0;
 }
 
-static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
-  KernelFn fn = pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant);
+static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, bool bf16) {
+  KernelFn fn = bf16 ? pick_kernel_bf16(d->a_layout, d->b_layout, d->a_op, d->b_op, variant)
+                     : pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant);
   if (!fn) {
     set_error("gemm: unsupported layout/op combination a=%d/%d b=%d/%d", d->a_layout, d->a_op, d->b_layout,
               d->b_op);
     return MDEMI_EUNSUP;
   }
   GemmParams p;
-  fill_params(d, p, variant);
+  fill_params(d, p, variant, bf16);
   float* rowsum_part = nullptr;
   if (p.split > 1) {
     const size_t need = slab_bytes(d, p) + rowsum_bytes(d, p) + colsum_combine_bytes(d, p);
@@ -807,14 +901,14 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st) {
                          rowsum_part ? d->rowsum_a : (float*)nullptr);
     }
   }
-  return check_launch("gemm_f32");
+  return check_launch(bf16 ? "gemm_bf16" : "gemm_f32");
 }
 
 struct TuneKey {
-  int al, bl, aop, bop, M, N, K, batch, split;
+  int al, bl, aop, bop, M, N, K, batch, split, bf16;
   bool operator<(const TuneKey& o) const {
-    return std::tie(al, bl, aop, bop, M, N, K, batch, split) <
-           std::tie(o.al, o.bl, o.aop, o.bop, o.M, o.N, o.K, o.batch, o.split);
+    return std::tie(al, bl, aop, bop, M, N, K, batch, split, bf16) <
+           std::tie(o.al, o.bl, o.aop, o.bop, o.M, o.N, o.K, o.batch, o.split, o.bf16);
   }
 };
 static std::map<TuneKey, int> g_tuned;
@@ -831,24 +925,28 @@ static bool tunable(const mdemi_gemm_desc* d, hipStream_t st) {
   return true;
 }
 
-static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st) {
-  if (g_variant >= 0) return g_variant;
-  const TuneKey key{d->a_layout, d->b_layout, d->a_op, d->b_op, d->M, d->N, d->K, d->batch, d->split_k};
+static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, bool bf16) {
+  if (bf16 ? g_variant_bf16 >= 0 : g_variant >= 0) return bf16 ? g_variant_bf16 : g_variant;
+  const TuneKey key{d->a_layout, d->b_layout, d->a_op, d->b_op, d->M, d->N, d->K, d->batch, d->split_k, (int)bf16};
   {
     std::lock_guard<std::mutex> lk(g_tune_mu);
     auto it = g_tuned.find(key);
     if (it != g_tuned.end()) return it->second;
   }
   if (!tunable(d, st)) return 0;
-  static const int cands[] = {0, 1, 3, 4, 5};
+  static const int cands_f32[] = {0, 1, 3, 4, 5};
+  static const int cands_bf16[] = {0, 1};
+  const int* cands = bf16 ? cands_bf16 : cands_f32;
+  const int ncand = bf16 ? 2 : 5;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 0;
   int best = 0;
   float best_ms = 1e30f;
-  for (int v : cands) {
-    if (launch(d, v, st) != MDEMI_OK) continue;  // warm (and validate)
+  for (int ci = 0; ci < ncand; ++ci) {
+    const int v = cands[ci];
+    if (launch(d, v, st, bf16) != MDEMI_OK) continue;  // warm (and validate)
     (void)hipEventRecord(e0, st);
-    for (int r = 0; r < 3; ++r) launch(d, v, st);
+    for (int r = 0; r < 3; ++r) launch(d, v, st, bf16);
     (void)hipEventRecord(e1, st);
     float ms = 0.f;
     if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
@@ -864,7 +962,11 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st) {
 extern "C" size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d) {
   if (!d || d->split_k <= 1) return 0;
   GemmParams p;
-  fill_params(d, p, 0);  // the split count does not depend on the variant
+  fill_params(d, p, 0, false);  // the split count does not depend on the variant
+  GemmParams pb;
+  fill_params(d, pb, 0, true);  // bf16 family: 64-element split chunks (never more splits)
+  if (p.split <= 1 && pb.split <= 1) return 0;
+  if (pb.split > p.split) p = pb;
   if (p.split <= 1) return 0;
   return slab_bytes(d, p) + rowsum_bytes(d, p) + colsum_combine_bytes(d, p);
 }
@@ -873,7 +975,14 @@ extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {
   int rc = validate(d);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  return launch(d, choose_variant(d, st), st);
+  return launch(d, choose_variant(d, st, false), st, false);
+}
+
+extern "C" int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream) {
+  int rc = validate(d);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  return launch(d, choose_variant(d, st, true), st, true);
 }
 
 // Benchmark/tuning hook: force a pipelining variant (see pick_variant; -1 =

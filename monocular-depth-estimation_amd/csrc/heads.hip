@@ -154,6 +154,18 @@ __global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ 
     y[i] = uniform01(seed, offset + (uint64_t)i) >= p ? x[i] * inv_keep : 0.f;
 }
 
+// the same mask with the seed read from device memory (seed_dev[0] + seed_add):
+// a seed drawn on the GPU by the caller changes on every replay of a captured
+// graph, where a host seed would be frozen into the kernel arguments
+__global__ __launch_bounds__(256) void dropout_dev_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                          int64_t n, float p, float inv_keep,
+                                                          const uint64_t* __restrict__ seed_dev, uint64_t seed_add,
+                                                          uint64_t offset) {
+  const uint64_t seed = seed_dev[0] + seed_add;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    y[i] = uniform01(seed, offset + (uint64_t)i) >= p ? x[i] * inv_keep : 0.f;
+}
+
 __global__ __launch_bounds__(256) void act_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
                                                       int act) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
@@ -475,6 +487,14 @@ extern "C" int mdemi_dropout(const float* x, float* y, int64_t n, float p, uint6
   }
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n, p, 1.f / (1.f - p), seed, offset);
   return check_launch("dropout");
+}
+
+extern "C" int mdemi_dropout_dev(const float* x, float* y, int64_t n, float p, const uint64_t* seed_dev,
+                                 uint64_t seed_add, uint64_t offset, void* stream) {
+  MDEMI_REQUIRE(x && y && n > 0 && p > 0.f && p < 1.f && seed_dev, "dropout_dev: bad args");
+  hipLaunchKernelGGL(dropout_dev_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, p,
+                     1.f / (1.f - p), seed_dev, seed_add, offset);
+  return check_launch("dropout_dev");
 }
 
 extern "C" int mdemi_act_fwd(const float* x, float* y, int64_t n, int32_t act, void* stream) {

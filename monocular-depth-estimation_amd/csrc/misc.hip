@@ -75,7 +75,9 @@ struct AdamGroups {
   mdemi_adamw_group g[4];
 };
 
-// per-tensor sum of squares partials: one block per (tensor, chunk)
+// per-tensor sum of squares partials: one block per (tensor, chunk); float4
+// loads over the 16-B-aligned body of the chunk (torch allocations are 256-B
+// aligned and chunks are multiples of 4 elements), scalar tail
 __global__ __launch_bounds__(OPT_THREADS) void sumsq_partial(const mdemi_tensor_ref* __restrict__ tl, int nt,
                                                              const int* __restrict__ chunk_tensor,
                                                              const int* __restrict__ chunk_index,
@@ -86,7 +88,13 @@ __global__ __launch_bounds__(OPT_THREADS) void sumsq_partial(const mdemi_tensor_
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
   const int64_t end = min(t.numel, beg + OPT_CHUNK);
   float s = 0.f;
-  for (int64_t i = beg + threadIdx.x; i < end; i += OPT_THREADS) s = fmaf(t.grad[i], t.grad[i], s);
+  const bool vec = ((uintptr_t)t.grad & 15) == 0;
+  const int64_t vend = vec ? beg + ((end - beg) & ~(int64_t)3) : beg;
+  for (int64_t i = beg + 4 * threadIdx.x; i < vend; i += 4 * OPT_THREADS) {
+    const float4 g = *reinterpret_cast<const float4*>(t.grad + i);
+    s = fmaf(g.x, g.x, s); s = fmaf(g.y, g.y, s); s = fmaf(g.z, g.z, s); s = fmaf(g.w, g.w, s);
+  }
+  for (int64_t i = vend + threadIdx.x; i < end; i += OPT_THREADS) s = fmaf(t.grad[i], t.grad[i], s);
   s = block_sum<OPT_THREADS>(s, red);
   if (threadIdx.x == 0) part[item] = s;
 }
@@ -104,42 +112,70 @@ __global__ void sumsq_final(const float* __restrict__ part, int nitems, float* _
   if (threadIdx.x == 0) out[0] = (float)red[0];
 }
 
+// torch.optim.AdamW on one (tensor, chunk) item (decoupled weight decay,
+// non-amsgrad, foreach=False semantics); `step` is the 1-based step count
+__device__ __forceinline__ void adamw_item(const mdemi_tensor_ref& t, const mdemi_adamw_group& gp, float clip,
+                                           float step, int64_t beg, int64_t end) {
+  const float b1 = gp.beta1, b2 = gp.beta2;
+  const float step_size = gp.lr / (1.f - powf(b1, step));
+  const float bc2s = sqrtf(1.f - powf(b2, step));
+  const float decay = 1.f - gp.lr * gp.weight_decay;
+  auto upd = [&](float g, float& p, float& m, float& v) {
+    g *= clip;
+    p *= decay;
+    m = m * b1 + (1.f - b1) * g;
+    v = v * b2 + (1.f - b2) * g * g;
+    p -= step_size * m / (sqrtf(v) / bc2s + gp.eps);
+  };
+  const bool vec = (((uintptr_t)t.param | (uintptr_t)t.grad | (uintptr_t)t.exp_avg | (uintptr_t)t.exp_avg_sq) & 15) == 0;
+  const int64_t vend = vec ? beg + ((end - beg) & ~(int64_t)3) : beg;
+  for (int64_t i = beg + 4 * threadIdx.x; i < vend; i += 4 * OPT_THREADS) {
+    const float4 g = *reinterpret_cast<const float4*>(t.grad + i);
+    float4 p = *reinterpret_cast<const float4*>(t.param + i);
+    float4 m = *reinterpret_cast<const float4*>(t.exp_avg + i);
+    float4 v = *reinterpret_cast<const float4*>(t.exp_avg_sq + i);
+    upd(g.x, p.x, m.x, v.x); upd(g.y, p.y, m.y, v.y); upd(g.z, p.z, m.z, v.z); upd(g.w, p.w, m.w, v.w);
+    *reinterpret_cast<float4*>(t.param + i) = p;
+    *reinterpret_cast<float4*>(t.exp_avg + i) = m;
+    *reinterpret_cast<float4*>(t.exp_avg_sq + i) = v;
+  }
+  for (int64_t i = vend + threadIdx.x; i < end; i += OPT_THREADS) upd(t.grad[i], t.param[i], t.exp_avg[i], t.exp_avg_sq[i]);
+}
+
+__device__ __forceinline__ float clip_coef(const float* sumsq, float max_norm) {
+  if (!(max_norm > 0.f) || !sumsq) return 1.f;
+  const float coef = max_norm / (sqrtf(sumsq[0]) + 1e-6f);
+  return coef < 1.f ? coef : 1.f;
+}
+
 __global__ __launch_bounds__(OPT_THREADS) void adamw_kernel(const mdemi_tensor_ref* __restrict__ tl,
                                                             const int* __restrict__ chunk_tensor,
                                                             const int* __restrict__ chunk_index, AdamGroups groups,
-                                                            const float* __restrict__ sumsq, float max_norm,
-                                                            float bc1, float bc2_sqrt_inv_dummy, int step) {
+                                                            const float* __restrict__ sumsq, float max_norm, int step) {
   const int item = blockIdx.x;
   const mdemi_tensor_ref t = tl[chunk_tensor[item]];
-  const mdemi_adamw_group gp = groups.g[t.group];
-  float clip = 1.f;
-  if (max_norm > 0.f && sumsq) {
-    const float total = sqrtf(sumsq[0]);
-    const float coef = max_norm / (total + 1e-6f);
-    clip = coef < 1.f ? coef : 1.f;
-  }
-  // torch.optim.AdamW (decoupled weight decay, non-amsgrad, foreach=False semantics)
-  const float b1 = gp.beta1, b2 = gp.beta2;
-  const float bias_c1 = 1.f - powf(b1, (float)step);
-  const float bias_c2 = 1.f - powf(b2, (float)step);
-  const float step_size = gp.lr / bias_c1;
-  const float bc2s = sqrtf(bias_c2);
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
-  const int64_t end = min(t.numel, beg + OPT_CHUNK);
-  (void)bc1; (void)bc2_sqrt_inv_dummy;
-  for (int64_t i = beg + threadIdx.x; i < end; i += OPT_THREADS) {
-    const float g = t.grad[i] * clip;
-    float p = t.param[i];
-    p *= 1.f - gp.lr * gp.weight_decay;
-    const float m = t.exp_avg[i] * b1 + (1.f - b1) * g;
-    const float v = t.exp_avg_sq[i] * b2 + (1.f - b2) * g * g;
-    t.exp_avg[i] = m;
-    t.exp_avg_sq[i] = v;
-    const float denom = sqrtf(v) / bc2s + gp.eps;
-    p -= step_size * m / denom;
-    t.param[i] = p;
-  }
+  adamw_item(t, groups.g[t.group], clip_coef(sumsq, max_norm), (float)step, beg, min(t.numel, beg + OPT_CHUNK));
 }
+
+// capturable form: hyperparameters of step s (= *step_dev, steps already taken)
+// from row min(s, nsteps - 1) of a device schedule table
+__global__ __launch_bounds__(OPT_THREADS) void adamw_dev_kernel(const mdemi_tensor_ref* __restrict__ tl,
+                                                                const int* __restrict__ chunk_tensor,
+                                                                const int* __restrict__ chunk_index,
+                                                                const mdemi_adamw_group* __restrict__ sched,
+                                                                int nsteps, int ngroups,
+                                                                const int* __restrict__ step_dev,
+                                                                const float* __restrict__ sumsq, float max_norm) {
+  const int item = blockIdx.x;
+  const mdemi_tensor_ref t = tl[chunk_tensor[item]];
+  const int s = step_dev[0];
+  const mdemi_adamw_group gp = sched[(int64_t)min(s, nsteps - 1) * ngroups + t.group];
+  const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
+  adamw_item(t, gp, clip_coef(sumsq, max_norm), (float)(s + 1), beg, min(t.numel, beg + OPT_CHUNK));
+}
+
+__global__ void step_tick_kernel(int* step_dev) { step_dev[0] += 1; }
 
 }  // namespace mdemi
 
@@ -216,8 +252,24 @@ extern "C" int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t nte
   const int* ct = (const int*)workspace;
   const int* ci = ct + nitems;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, (hipStream_t)stream, tensors_dev, ct,
-                     ci, g, sumsq, max_norm, 0.f, 0.f, step);
+                     ci, g, sumsq, max_norm, step);
   return check_launch("adamw_step");
+}
+
+extern "C" int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
+                                    const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
+                                    int32_t* step_dev, const float* sumsq, float max_norm, int64_t nitems,
+                                    void* workspace, void* stream) {
+  MDEMI_REQUIRE(tensors_dev && ntensors > 0 && sched_dev && nsteps > 0 && ngroups > 0 && ngroups <= 4 && step_dev &&
+                    nitems > 0 && workspace,
+                "adamw_step_dev: bad args");
+  const int* ct = (const int*)workspace;
+  const int* ci = ct + nitems;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adamw_dev_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, st, tensors_dev, ct, ci, sched_dev,
+                     nsteps, ngroups, (const int*)step_dev, sumsq, max_norm);
+  hipLaunchKernelGGL(step_tick_kernel, dim3(1), dim3(1), 0, st, (int*)step_dev);
+  return check_launch("adamw_step_dev");
 }
 
 // Stochastic depth (timm DropPath, swin_transformer.py:181,243-244):

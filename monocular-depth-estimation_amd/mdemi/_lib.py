@@ -101,6 +101,7 @@ _SIGS = {
     "mdemi_version": (ctypes.c_int, []),
     "mdemi_gemm_workspace_size": (sz, [ctypes.POINTER(GemmDesc)]),
     "mdemi_gemm_f32": (ctypes.c_int, [ctypes.POINTER(GemmDesc), vp]),
+    "mdemi_gemm_bf16": (ctypes.c_int, [ctypes.POINTER(GemmDesc), vp]),
     "mdemi_gemm_set_variant": (ctypes.c_int, [i32, i32]),
     "mdemi_colsum_workspace_size": (sz, [i64, i64]),
     "mdemi_colsum_f32": (ctypes.c_int, [vp, i64, i64, i64, vp, ctypes.c_int, vp, vp]),
@@ -143,6 +144,7 @@ _SIGS = {
     "mdemi_grad_norm_workspace_size": (sz, [i32]),
     "mdemi_grad_sumsq": (ctypes.c_int, [vp, i32, i64, vp, vp, vp]),
     "mdemi_adamw_step": (ctypes.c_int, [vp, i32, ctypes.POINTER(AdamWGroup), i32, vp, f32, i32, i64, vp, vp]),
+    "mdemi_adamw_step_dev": (ctypes.c_int, [vp, i32, vp, i32, i32, vp, vp, f32, i64, vp, vp]),
     # ---- include/mdemi_ext.h ----
     "mdemi_dwconv_fwd": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mdemi_dwconv_bwd_workspace_size": (sz, [i32, i32, i32, i32, i32]),
@@ -158,6 +160,7 @@ _SIGS = {
     "mdemi_softmax_bwd": (ctypes.c_int, [vp, vp, vp, i64, i32, f32, i32, vp]),
     "mdemi_act_fwd": (ctypes.c_int, [vp, vp, i64, i32, vp]),
     "mdemi_dropout": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_uint64, ctypes.c_uint64, vp]),
+    "mdemi_dropout_dev": (ctypes.c_int, [vp, vp, i64, f32, vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "mdemi_binhead_nhwc_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, vp]),
     "mdemi_binhead_nhwc_bwd_workspace_size": (sz, [i32, i64, i32]),
     "mdemi_binhead_nhwc_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, vp, vp]),
@@ -236,6 +239,10 @@ def stream() -> int:
 
 # ---- per-device scratch (the library never allocates) ----
 _ws: dict = {}
+# Every workspace buffer ever handed out stays alive: a captured hipGraph keeps
+# the raw addresses it was recorded with, so a buffer superseded by a larger one
+# (a later eager call at a bigger shape) must never return to the allocator.
+_ws_retired: list = []
 
 
 def workspace(nbytes: int, device=None, slot: int = 0) -> torch.Tensor:
@@ -246,6 +253,11 @@ def workspace(nbytes: int, device=None, slot: int = 0) -> torch.Tensor:
     buf = _ws.get(key)
     nbytes = max(int(nbytes), 256)
     if buf is None or buf.numel() < nbytes:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"mdemi: workspace slot {slot} must grow to {nbytes} bytes during hipGraph capture; "
+                               "run the captured step eagerly first (warm-up) so every workspace is sized")
+        if buf is not None:
+            _ws_retired.append(buf)
         buf = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=device)
         _ws[key] = buf
     return buf

@@ -50,6 +50,49 @@ def _split_for(M, N, K):
     return max(1, split)
 
 
+def _draw_seed(device):
+    """A dropout seed drawn on the GPU (torch's Philox; graph-safe: a captured step draws a new
+    one on every replay).  Kernels read it through mdemi_dropout_dev."""
+    return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
+
+
+def _drop(src_ptr, dst_ptr, n, p, seed, add=0, offset=0):
+    """Inverted dropout of n floats; mask = hash(seed[0] + add, offset + i)."""
+    L.call("mdemi_dropout_dev", src_ptr, dst_ptr, n, float(p), seed.data_ptr(), add, offset, L.stream())
+
+
+# Matmul precision of every libmdemi GEMM: "fp32" (exact fp32 MFMA, the reference's
+# precision) or "bf16" (bf16 operands, fp32 accumulate: torch.autocast's matmul numerics,
+# BASELINE configs[4]).  Process-wide; set it for a whole train step (forward and backward).
+_PRECISION = ["fp32"]
+
+
+def set_matmul_precision(precision: str) -> None:
+    if precision not in ("fp32", "bf16"):
+        raise ValueError(f"matmul precision must be 'fp32' or 'bf16', got {precision!r}")
+    _PRECISION[0] = precision
+
+
+def get_matmul_precision() -> str:
+    return _PRECISION[0]
+
+
+class matmul_precision:
+    """Context manager: with matmul_precision("bf16"): ..."""
+
+    def __init__(self, precision):
+        self.precision, self.prev = precision, None
+
+    def __enter__(self):
+        self.prev = get_matmul_precision()
+        set_matmul_precision(self.precision)
+        return self
+
+    def __exit__(self, *a):
+        set_matmul_precision(self.prev)
+        return False
+
+
 def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE, b_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
@@ -77,7 +120,10 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     if need:
         ws = L.workspace(need, C.device, slot=1)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
-    L.check(lib.mdemi_gemm_f32(ctypes.byref(d), L.stream()), "gemm_f32")
+    if _PRECISION[0] == "bf16":
+        L.check(lib.mdemi_gemm_bf16(ctypes.byref(d), L.stream()), "gemm_bf16")
+    else:
+        L.check(lib.mdemi_gemm_f32(ctypes.byref(d), L.stream()), "gemm_f32")
     return C
 
 
@@ -182,12 +228,11 @@ class _MlpFn(torch.autograd.Function):
              bias=b1, bias_mode=L.BIAS_COL if b1 is not None else L.BIAS_NONE, act=act,
              preact=h, ldpre=Hd, split_k=1)
         if p_mid > 0.0:
-            L.call("mdemi_dropout", g.data_ptr(), g.data_ptr(), g.numel(), float(p_mid), seed, 0, L.stream())
+            _drop(g.data_ptr(), g.data_ptr(), g.numel(), p_mid, seed)
         res2 = _c(residual).reshape(M, N) if residual is not None else None
         if p_out > 0.0:
             out = linear_fwd_raw(g, _c(w2), b2)
-            L.call("mdemi_dropout", out.data_ptr(), out.data_ptr(), out.numel(), float(p_out), seed + 1, 0,
-                   L.stream())
+            _drop(out.data_ptr(), out.data_ptr(), out.numel(), p_out, seed, add=1)
             if res2 is not None:
                 L.call("mdemi_elementwise", L.EW_ADD, out.data_ptr(), res2.data_ptr(), out.data_ptr(), out.numel(),
                        0.0, 0.0, L.stream())
@@ -210,7 +255,7 @@ class _MlpFn(torch.autograd.Function):
         dev = dy.device
         if p_out > 0.0:
             d2 = torch.empty_like(dy2)
-            L.call("mdemi_dropout", dy2.data_ptr(), d2.data_ptr(), d2.numel(), float(p_out), seed + 1, 0, L.stream())
+            _drop(dy2.data_ptr(), d2.data_ptr(), d2.numel(), p_out, seed, add=1)
         else:
             d2 = dy2
         dw2 = torch.empty(N, Hd, device=dev, dtype=torch.float32)
@@ -220,7 +265,7 @@ class _MlpFn(torch.autograd.Function):
         dh = torch.empty(M, Hd, device=dev, dtype=torch.float32)
         if p_mid > 0.0:
             gemm(d2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
-            L.call("mdemi_dropout", dh.data_ptr(), dh.data_ptr(), dh.numel(), float(p_mid), seed, 0, L.stream())
+            _drop(dh.data_ptr(), dh.data_ptr(), dh.numel(), p_mid, seed)
             L.call("mdemi_elementwise", L.EW_ACT_BWD, h.data_ptr(), dh.data_ptr(), dh.data_ptr(), dh.numel(),
                    float(act), 0.0, L.stream())
         else:
@@ -244,7 +289,7 @@ def mlp(x, w1, b1, w2, b2, residual=None, act=L.ACT_GELU, p_mid=0.0, p_out=0.0, 
     """fc2(dropout(act(fc1(x)))) -> dropout (+ residual); act GELU (exact erf), SiLU or ReLU."""
     if not training:
         p_mid = p_out = 0.0
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (p_mid > 0.0 or p_out > 0.0) else 0
+    seed = _draw_seed(x.device) if (p_mid > 0.0 or p_out > 0.0) else None
     return _MlpFn.apply(x, w1, b1, w2, b2, residual, (act, float(p_mid), float(p_out), seed))
 
 
@@ -1250,7 +1295,7 @@ class _DropoutFn(torch.autograd.Function):
         _require_cuda(x)
         x = _c(x)
         y = torch.empty_like(x)
-        L.call("mdemi_dropout", x.data_ptr(), y.data_ptr(), x.numel(), float(p), seed, offset, L.stream())
+        _drop(x.data_ptr(), y.data_ptr(), x.numel(), p, seed, offset=offset)
         ctx.cfg = (p, seed, offset)
         return y
 
@@ -1259,16 +1304,16 @@ class _DropoutFn(torch.autograd.Function):
         p, seed, offset = ctx.cfg
         dy = _c(dy)
         dx = torch.empty_like(dy)
-        L.call("mdemi_dropout", dy.data_ptr(), dx.data_ptr(), dy.numel(), float(p), seed, offset, L.stream())
+        _drop(dy.data_ptr(), dx.data_ptr(), dy.numel(), p, seed, offset=offset)
         return dx, None, None, None
 
 
 def dropout(x, p, training):
-    """Inverted dropout; the mask is a hash of (seed, element index), drawn from torch's CPU generator
-    once per call, so the backward regenerates it instead of storing it."""
+    """Inverted dropout; the mask is a hash of (seed, element index) with the seed drawn on the
+    GPU once per call, so the backward regenerates it instead of storing it."""
     if not training or p == 0.0:
         return x
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    seed = _draw_seed(x.device)
     off = _drop_counter[0]
     _drop_counter[0] += x.numel()
     return _DropoutFn.apply(x, p, seed, off)
@@ -1484,7 +1529,7 @@ class _AttentionFn(torch.autograd.Function):
         Pd = P
         if p > 0.0:
             Pd = torch.empty_like(P)
-            L.call("mdemi_dropout", P.data_ptr(), Pd.data_ptr(), P.numel(), float(p), seed, 0, L.stream())
+            _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed)
         out = torch.empty(B * Sq, heads * dv, device=dev, dtype=torch.float32)
         for h in range(heads):
             gemm(Pd, vsrc, out, Sq, dv, Sk, lda=Sk, ldb=ldv, ldc=heads * dv, a_layout=L.L_KCONTIG,
@@ -1503,7 +1548,7 @@ class _AttentionFn(torch.autograd.Function):
         Pd = P
         if p > 0.0:
             Pd = torch.empty_like(P)
-            L.call("mdemi_dropout", P.data_ptr(), Pd.data_ptr(), P.numel(), float(p), seed, 0, L.stream())
+            _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed)
         # one gradient buffer per distinct source tensor; columns outside the used slices are zero
         bufs, spans = {}, {}
         for t, off, width in ((qsrc, q_off, heads * dqk), (ksrc, k_off, heads * dqk), (vsrc, v_off, heads * dv)):
@@ -1526,7 +1571,7 @@ class _AttentionFn(torch.autograd.Function):
                      b_layout=L.L_MNCONTIG, batch=B, a_bstride=heads * hs, b_bstride=Sq * heads * dv,
                      c_bstride=Sk * ldv, a_off=h * hs, b_off=h * dv, c_off=v_off + h * dv)
             if p > 0.0:
-                L.call("mdemi_dropout", dP.data_ptr(), dP.data_ptr(), dP.numel(), float(p), seed, 0, L.stream())
+                _drop(dP.data_ptr(), dP.data_ptr(), dP.numel(), p, seed)
             if dP_ext is not None:
                 dP_ext = _c(dP_ext)
                 L.call("mdemi_elementwise", L.EW_ADD, dP.data_ptr(), dP_ext.data_ptr(), dP.data_ptr(), dP.numel(),
@@ -1557,7 +1602,7 @@ def attention(qsrc, ksrc, vsrc, B, Sq, Sk, heads, dqk, dv, scale, q_off=0, k_off
     (offsets q_off/k_off/v_off, head-major) of 2-D token-major buffers [B*S, ld]; a buffer may
     feed several of them (e.g. a fused qkv projection)."""
     p = float(p) if training else 0.0
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0.0 else 0
+    seed = _draw_seed(qsrc.device) if p > 0.0 else None
     cfg = (B, Sq, Sk, heads, dqk, dv, q_off, k_off, v_off, float(scale), p, seed)
     return _AttentionFn.apply(_c(qsrc), _c(ksrc), _c(vsrc), cfg)
 

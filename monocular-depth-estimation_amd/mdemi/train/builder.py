@@ -103,12 +103,12 @@ def param_groups(model, opt):
     return [{"params": list(model.parameters()), "lr": lr}]
 
 
-def build_optimizer(model, opt):
+def build_optimizer(model, opt, capturable=False):
     o = opt.get("optimizer", {})
     betas = tuple(float(b) for b in o.get("betas", (0.9, 0.999)))
     return FusedAdamW(param_groups(model, opt), lr=float(o["lr"]), betas=betas, eps=float(o.get("eps", 1e-8)),
                       weight_decay=float(o.get("weight_decay", 0.0)),
-                      max_grad_norm=float(opt.get("train", {}).get("grad_norm", 0.0)))
+                      max_grad_norm=float(opt.get("train", {}).get("grad_norm", 0.0)), capturable=capturable)
 
 
 def optimizer_steps_per_epoch(opt, world=1, images=None):
@@ -141,9 +141,19 @@ def freeze_bn(model):
 class Trainer:
     """One optimizer step = num_accum micro-batches of forward + loss/num_accum + backward
     (gradients accumulate in place), then the gradient all-reduce (DDP), the clipped
-    AdamW update and one OneCycle step."""
+    AdamW update and one OneCycle step.
 
-    def __init__(self, opt, model, criterion, optimizer, scheduler, ddp=None):
+    precision "bf16": every libmdemi GEMM (Linear, conv, attention products; forward and
+    backward) runs with bf16 operands and fp32 accumulation -- torch.autocast's matmul
+    numerics -- while master weights, optimizer state and the other kernels stay fp32.
+    graph=True: the first two calls run eagerly (they settle GEMM autotuning, every
+    workspace and the optimizer state; gradients stay allocated), the third captures the
+    whole step -- forward, loss, backward, clip, AdamW with its schedule read on the
+    device -- into a hipGraph (torch.cuda.CUDAGraph) and replays it; every later call copies
+    its batch into the static input buffers and replays.  Each call is exactly one
+    optimizer step.  Dropout seeds are drawn on the GPU, so masks differ per replay."""
+
+    def __init__(self, opt, model, criterion, optimizer, scheduler, ddp=None, precision="fp32", graph=False):
         tr = opt.get("train", {})
         self.opt, self.model, self.criterion = opt, model, criterion
         self.optimizer, self.scheduler, self.ddp = optimizer, scheduler, ddp
@@ -151,6 +161,19 @@ class Trainer:
         self.freeze_encoder_bn = bool(tr.get("freeze_encoder_bn", False))
         self.freeze_all_bn = int(tr.get("freeze_all_bn", -1))
         self.epoch = 0
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.precision = precision
+        self.graph = bool(graph)
+        if self.graph:
+            if ddp is not None:
+                raise NotImplementedError("graph capture of the data-parallel step is not built (use graph=False)")
+            if not getattr(optimizer, "capturable", False):
+                raise ValueError("graph=True needs FusedAdamW(capturable=True)")
+            if scheduler is not None:
+                optimizer.set_schedule(scheduler.hyper_table())
+        self._graph = None
+        self._eager_calls = 0
 
     def train_mode(self):
         self.model.train()
@@ -165,6 +188,50 @@ class Trainer:
         if len(batches) != self.num_accum:
             raise ValueError(f"Trainer.step: expected {self.num_accum} micro-batches (train.num_accum), "
                              f"got {len(batches)}")
+        from .. import functional as mf
+        if self.graph:
+            return self._graph_step(batches)
+        with mf.matmul_precision(self.precision):
+            return self._eager_step(batches)
+
+    def _graph_step(self, batches):
+        from .. import functional as mf
+        if self._graph is None:
+            if self._eager_calls < 2:  # warm-up: autotuning, workspaces, optimizer state
+                self._eager_calls += 1
+                with mf.matmul_precision(self.precision):
+                    return self._eager_step(batches)
+            self._static = [(img.clone(), gt.clone()) for img, gt in batches]
+            self.optimizer.zero_grad(set_to_none=False)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g), mf.matmul_precision(self.precision):
+                self._static_loss = self._body(self._static)
+            self.optimizer.step_count -= 1  # capture records the step, it does not run it
+            self._graph = g
+        else:
+            for (si, sg), (img, gt) in zip(self._static, batches):
+                si.copy_(img, non_blocking=True)
+                sg.copy_(gt, non_blocking=True)
+        self._graph.replay()
+        self.optimizer.step_count += 1  # host mirror of the device step counter
+        if self.scheduler is not None:
+            self.scheduler.step()
+        return self._static_loss
+
+    def _body(self, batches):
+        """The captured step: no host synchronisation, no host-side hyperparameters."""
+        total = None
+        for img, gt in batches:
+            loss = self.criterion(self.model(img), gt)
+            if self.num_accum > 1:
+                loss = loss * (1.0 / self.num_accum)
+            loss.backward()
+            total = loss.detach() if total is None else total + loss.detach()
+        self.optimizer.step()
+        self.optimizer.zero_grad(set_to_none=False)  # gradients keep their (captured) addresses
+        return total
+
+    def _eager_step(self, batches):
         total = None
         for i, (img, gt) in enumerate(batches):
             last = i == len(batches) - 1
@@ -183,7 +250,7 @@ class Trainer:
         if self.ddp is not None:
             self.ddp.zero_grad()
         else:
-            self.optimizer.zero_grad(set_to_none=True)
+            self.optimizer.zero_grad(set_to_none=not self.graph)
         return total
 
 
@@ -195,10 +262,13 @@ class _null:
         return False
 
 
-def build_from_config(opt, device=None, world=1, steps_per_epoch=None, ddp_bucket_mb=64.0, drop_path=None):
+def build_from_config(opt, device=None, world=1, steps_per_epoch=None, ddp_bucket_mb=64.0, drop_path=None,
+                      precision=None, graph=False):
     """opt (parse()'s dict) -> Trainer.  device='meta' builds every object without
     allocating parameters (config validation); world > 1 wraps the gradients in the
-    bucketed RCCL all-reduce (needs an initialised process group)."""
+    bucketed RCCL all-reduce (needs an initialised process group).  precision
+    (default: train.precision or "fp32") and graph select the mixed-precision /
+    hipGraph-captured step (Trainer)."""
     name = opt["model"]["name"]
     if device is not None and torch.device(device).type == "meta":
         with torch.device("meta"):
@@ -208,7 +278,7 @@ def build_from_config(opt, device=None, world=1, steps_per_epoch=None, ddp_bucke
         if device is not None:
             model = model.to(device)
     criterion = TrainLoss(opt, name)
-    optimizer = build_optimizer(model, opt)
+    optimizer = build_optimizer(model, opt, capturable=graph)
     spe = steps_per_epoch if steps_per_epoch is not None else optimizer_steps_per_epoch(opt, world)
     scheduler = build_scheduler(optimizer, opt, spe)
     ddp = None
@@ -216,6 +286,7 @@ def build_from_config(opt, device=None, world=1, steps_per_epoch=None, ddp_bucke
         from .ddp import GradAllReduce, broadcast_parameters
         broadcast_parameters(model)
         ddp = GradAllReduce(model, bucket_mb=ddp_bucket_mb)
-    trainer = Trainer(opt, model, criterion, optimizer, scheduler, ddp)
+    precision = precision or opt.get("train", {}).get("precision", "fp32")
+    trainer = Trainer(opt, model, criterion, optimizer, scheduler, ddp, precision=precision, graph=graph)
     trainer.train_mode()
     return trainer

@@ -14,9 +14,16 @@ from .. import _lib as L
 
 class FusedAdamW:
     """torch.optim.AdamW semantics (decoupled weight decay, amsgrad=False) for fp32
-    CUDA params; one gradient-norm kernel + one update kernel per step, no host sync."""
+    CUDA params; one gradient-norm kernel + one update kernel per step, no host sync.
 
-    def __init__(self, param_groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, max_grad_norm=0.0):
+    capturable=True: the per-step hyperparameters (lr, betas, bias-correction step) are
+    read on the device from a schedule table (set_schedule; default: the groups' current
+    values) indexed by a device step counter, so the whole step can live in a captured
+    hipGraph (mdemi_adamw_step_dev).  The host mirror (step_count, param_groups) is
+    advanced by the caller on each replay (Trainer does)."""
+
+    def __init__(self, param_groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, max_grad_norm=0.0,
+                 capturable=False):
         if isinstance(param_groups, torch.Tensor) or (isinstance(param_groups, (list, tuple)) and param_groups and
                                                       isinstance(param_groups[0], torch.Tensor)):
             param_groups = [{"params": list(param_groups)}]
@@ -39,6 +46,31 @@ class FusedAdamW:
         self.step_count = 0
         self._chunk = L.load().mdemi_multi_tensor_chunk()
         self._sumsq = None
+        self.capturable = bool(capturable)
+        self._sched_rows = None  # host schedule [(lr, beta1, beta2, eps, wd) per group] per step
+        self._sched_dev = None
+        self._step_dev = None
+
+    # ---- capturable schedule ----
+    def set_schedule(self, rows):
+        """rows[s][g] = (lr, beta1, beta2, eps, weight_decay) used by optimizer step s (0-based)."""
+        if not rows or any(len(r) != len(self.param_groups) for r in rows):
+            raise ValueError("FusedAdamW.set_schedule: one row per step, one entry per parameter group")
+        self._sched_rows = [[tuple(float(v) for v in e) for e in r] for r in rows]
+        self._sched_dev = None
+
+    def _device_schedule(self, dev, taken):
+        """taken: optimizer steps completed before the one being launched."""
+        if self._sched_dev is None:
+            rows = self._sched_rows
+            if rows is None:  # constant hyperparameters: the groups' current values
+                rows = [[(g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"])
+                         for g in self.param_groups]]
+            flat = [v for r in rows for e in r for v in (*e, 0.0)]  # mdemi_adamw_group: 5 floats + pad
+            t = torch.tensor(flat, dtype=torch.float32)
+            self._sched_dev = (t.to(dev), len(rows))
+            self._step_dev = torch.full((1,), taken, dtype=torch.int32, device=dev)
+        return self._sched_dev
 
     def zero_grad(self, set_to_none=True):
         for g in self.param_groups:
@@ -73,47 +105,89 @@ class FusedAdamW:
 
     @torch.no_grad()
     def step(self):
-        refs, items_t, items_c = self._refs()
-        if not refs:
+        params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+        if not params:
             return
         self.step_count += 1
         dev = torch.device("cuda", torch.cuda.current_device())
-        nt, ni = len(refs), len(items_t)
         lib = L.load()
-        # one host->device copy per step: [TensorRef x nt | chunk_tensor | chunk_index | partials]
-        raw = (L.TensorRef * nt)(*refs)
-        rb = (ctypes.sizeof(raw) + 255) // 256 * 256
-        wsb = lib.mdemi_grad_norm_workspace_size(ni)
-        host = torch.empty(rb + wsb, dtype=torch.uint8, pin_memory=True)
-        ctypes.memmove(host.data_ptr(), ctypes.addressof(raw), ctypes.sizeof(raw))
-        host[rb:rb + 8 * ni].view(torch.int32).copy_(torch.tensor(items_t + items_c, dtype=torch.int32))
-        dev_buf = host.to(dev, non_blocking=True)
-        tl_ptr, ws_ptr = dev_buf.data_ptr(), dev_buf.data_ptr() + rb
+        # device table of (param, grad, state) pointers: rebuilt only when a .grad moved
+        # (set_to_none), so a step with persistent gradients (captured graphs, DDP bucket
+        # views) issues no host->device copy at all
+        key = tuple(p.grad.data_ptr() for p in params)
+        if key != getattr(self, "_tbl_key", None):
+            refs, items_t, items_c = self._refs()
+            nt, ni = len(refs), len(items_t)
+            raw = (L.TensorRef * nt)(*refs)
+            rb = (ctypes.sizeof(raw) + 255) // 256 * 256
+            wsb = lib.mdemi_grad_norm_workspace_size(ni)
+            host = torch.empty(rb + wsb, dtype=torch.uint8, pin_memory=True)
+            ctypes.memmove(host.data_ptr(), ctypes.addressof(raw), ctypes.sizeof(raw))
+            host[rb:rb + 8 * ni].view(torch.int32).copy_(torch.tensor(items_t + items_c, dtype=torch.int32))
+            dev_buf = host.to(dev, non_blocking=True)
+            self._tbl = (host, dev_buf, dev_buf.data_ptr(), dev_buf.data_ptr() + rb, nt, ni)
+            self._tbl_key = key
+        _, _, tl_ptr, ws_ptr, nt, ni = self._tbl
         if self._sumsq is None:
             self._sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
         if self.max_grad_norm > 0:
             L.check(lib.mdemi_grad_sumsq(tl_ptr, nt, ni, self._sumsq.data_ptr(), ws_ptr, L.stream()), "grad_sumsq")
-        groups = (L.AdamWGroup * len(self.param_groups))()
-        for i, g in enumerate(self.param_groups):
-            groups[i].lr, (groups[i].beta1, groups[i].beta2) = g["lr"], g["betas"]
-            groups[i].eps, groups[i].weight_decay = g["eps"], g["weight_decay"]
-        L.check(lib.mdemi_adamw_step(tl_ptr, nt, groups, len(self.param_groups),
-                                     self._sumsq.data_ptr() if self.max_grad_norm > 0 else None,
-                                     self.max_grad_norm, self.step_count, ni, ws_ptr, L.stream()), "adamw_step")
-        self._keepalive = (host, dev_buf)
+        clip = self._sumsq.data_ptr() if self.max_grad_norm > 0 else None
+        if self.capturable:
+            sched, nsteps = self._device_schedule(dev, self.step_count - 1)
+            L.check(lib.mdemi_adamw_step_dev(tl_ptr, nt, sched.data_ptr(), nsteps, len(self.param_groups),
+                                             self._step_dev.data_ptr(), clip, self.max_grad_norm, ni, ws_ptr,
+                                             L.stream()), "adamw_step_dev")
+        else:
+            groups = (L.AdamWGroup * len(self.param_groups))()
+            for i, g in enumerate(self.param_groups):
+                groups[i].lr, (groups[i].beta1, groups[i].beta2) = g["lr"], g["betas"]
+                groups[i].eps, groups[i].weight_decay = g["eps"], g["weight_decay"]
+            L.check(lib.mdemi_adamw_step(tl_ptr, nt, groups, len(self.param_groups), clip, self.max_grad_norm,
+                                         self.step_count, ni, ws_ptr, L.stream()), "adamw_step")
 
     def state_dict(self):
-        return {"step": self.step_count,
-                "state": {i: v for i, v in enumerate(self.state.values())},
-                "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]}
+        """torch.optim.AdamW's layout: state keyed by each parameter's position across
+        param_groups (not by the order gradients first appeared), a per-parameter "step",
+        and "params" index lists per group -- so save_checkpoint files
+        (common_utils.py:12-31 optimizer_state_dict) round-trip with torch's AdamW."""
+        state, groups, idx = {}, [], 0
+        for g in self.param_groups:
+            ids = []
+            for p in g["params"]:
+                st = self.state.get(p)
+                if st is not None:
+                    state[idx] = {"step": torch.tensor(float(self.step_count)), "exp_avg": st["exp_avg"],
+                                  "exp_avg_sq": st["exp_avg_sq"]}
+                ids.append(idx)
+                idx += 1
+            gd = {k: v for k, v in g.items() if k != "params"}
+            gd.update(amsgrad=False, maximize=False, foreach=None, capturable=self.capturable,
+                      differentiable=False, fused=None, params=ids)
+            groups.append(gd)
+        return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd):
-        self.step_count = sd["step"]
         params = [p for g in self.param_groups for p in g["params"]]
+        if len(sd["param_groups"]) != len(self.param_groups):
+            raise ValueError("loaded state dict has a different number of parameter groups")
+        order = [i for sg in sd["param_groups"] for i in sg["params"]]
+        if len(order) != len(params):
+            raise ValueError("loaded state dict contains a parameter group that doesn't match the size of the "
+                             "optimizer's group")
+        pos = {int(i): params[k] for k, i in enumerate(order)}
+        self.state = {}
+        steps = [0]
         for i, v in sd["state"].items():
-            self.state[params[int(i)]] = {k: t.to(params[int(i)].device) for k, t in v.items()}
+            p = pos[int(i)]
+            self.state[p] = {k: v[k].detach().to(p.device, torch.float32).clone() for k in ("exp_avg", "exp_avg_sq")}
+            steps.append(int(float(v.get("step", 0))))
+        self.step_count = max(steps)
         for g, sg in zip(self.param_groups, sd["param_groups"]):
-            g.update({k: v for k, v in sg.items()})
+            g.update({k: v for k, v in sg.items() if k in ("lr", "betas", "eps", "weight_decay", "initial_lr",
+                                                          "max_lr", "min_lr", "max_momentum", "base_momentum")})
+        self._tbl_key = None
+        self._sched_dev = None
 
 
 class OneCycleLR:
@@ -142,21 +216,38 @@ class OneCycleLR:
     def _cos(start, end, pct):
         return end + (start - end) / 2.0 * (math.cos(math.pi * pct) + 1)
 
+    def values(self, s, g):
+        """(lr, beta1) of parameter group g after s scheduler steps."""
+        start = 0.0
+        for i, (end, lr0, lr1, m0, m1) in enumerate(self.phases):
+            if s <= end or i == len(self.phases) - 1:
+                pct = (s - start) / (end - start) if end > start else 0.0
+                lr = self._cos(g[lr0], g[lr1], pct)
+                b1 = self._cos(g[m0], g[m1], pct) if self.cycle_momentum else g["betas"][0]
+                return lr, b1
+            start = end
+
     def step(self):
         self.last_step += 1
         s = self.last_step
         if s > self.total:
             raise ValueError(f"OneCycleLR stepped {s} times; total_steps={self.total}")
         for g in self.opt.param_groups:
-            start = 0.0
-            for i, (end, lr0, lr1, m0, m1) in enumerate(self.phases):
-                if s <= end or i == len(self.phases) - 1:
-                    pct = (s - start) / (end - start) if end > start else 0.0
-                    g["lr"] = self._cos(g[lr0], g[lr1], pct)
-                    if self.cycle_momentum:
-                        g["betas"] = (self._cos(g[m0], g[m1], pct), g["betas"][1])
-                    break
-                start = end
+            g["lr"], b1 = self.values(s, g)
+            g["betas"] = (b1, g["betas"][1])
+
+    def hyper_table(self):
+        """Row s = (lr, beta1, beta2, eps, weight_decay) per group after s scheduler steps,
+        s = 0..total: FusedAdamW.set_schedule's rows for a captured train step (the optimizer
+        and the scheduler step together, so row s serves optimizer step s)."""
+        rows = []
+        for s in range(self.total + 1):
+            row = []
+            for g in self.opt.param_groups:
+                lr, b1 = self.values(s, g)
+                row.append((lr, b1, g["betas"][1], g["eps"], g["weight_decay"]))
+            rows.append(row)
+        return rows
 
     def get_last_lr(self):
         return [g["lr"] for g in self.opt.param_groups]

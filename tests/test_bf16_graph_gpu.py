@@ -1,0 +1,210 @@
+"""Mixed precision (bf16 operands, fp32 accumulate) and the hipGraph-captured train step
+(BASELINE configs[4]: Depthformer bf16 + hipGraph).
+
+* mdemi_gemm_bf16 on every operand layout (dense, implicit-im2col conv, GELU-on-load,
+  split-K, bias-gradient row sums) against fp64 products of the same operands rounded to
+  bf16: the only difference allowed is fp32 accumulation order (stated tolerance below).
+* The Depthformer v8 decoder + bin head under bf16 against the reference's golden vectors
+  (tests/golden/depthformer_v8.npz): bf16 tolerance stated in the test.
+* A captured train step replays bit-for-bit what the eager step computes (dropout off),
+  and with dropout on every replay draws new masks."""
+import copy
+
+import pytest
+import torch
+
+from golden_util import Golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+# fp32 accumulation of exact bf16 x bf16 products: |err| <= ACC_RTOL * max_ij sum_k |a_ik b_kj|
+ACC_RTOL = 2e-6
+# bf16 model vs the fp32 reference (8-bit-mantissa GEMM operands through the whole decoder):
+# relative L2 error per tensor
+# (measured: outputs <= 1e-3, gradients <= 7e-2 -- BatchNorm affine gradients, sums of
+# dY x-hat over every pixel, carry the largest bf16 error)
+BF16_OUT_L2, BF16_GRAD_L2 = 1e-2, 1e-1
+
+
+@pytest.fixture(scope="module")
+def mf():
+    from mdemi import _lib
+    from mdemi import functional
+    _lib.load()
+    return functional
+
+
+def _r16(t):
+    return t.to(torch.bfloat16).double()
+
+
+def _check_acc(got, ref_rounded, absprod, what):
+    err = (got.double().cpu() - ref_rounded).abs().max().item()
+    lim = ACC_RTOL * absprod.max().item() + 1e-30
+    assert err <= lim, (what, err, lim)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 96), (1000, 384, 1536), (64, 96, 40000)])
+def test_linear_bf16_fwd_dgrad_wgrad(mf, M, N, K):
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV, requires_grad=True)
+    w = (torch.randn(N, K, device=DEV) * 0.05).requires_grad_()
+    b = torch.randn(N, device=DEV, requires_grad=True)
+    dy = torch.randn(M, N, device=DEV)
+    with mf.matmul_precision("bf16"):
+        y = mf.linear(x, w, b)
+        y.backward(dy)
+    xd, wd, dyd = x.detach().cpu(), w.detach().cpu(), dy.cpu()
+    _check_acc(y.detach() - b.detach(), _r16(xd) @ _r16(wd).T, xd.double().abs() @ wd.double().abs().T, "fwd")
+    _check_acc(x.grad, _r16(dyd) @ _r16(wd), dyd.double().abs() @ wd.double().abs(), "dgrad")
+    _check_acc(w.grad, _r16(dyd).T @ _r16(xd), dyd.double().abs().T @ xd.double().abs(), "wgrad")
+    # the bias gradient is summed from the unrounded fp32 dY
+    assert torch.allclose(b.grad.double().cpu(), dyd.double().sum(0), rtol=1e-5, atol=1e-4)
+    # and bf16 really is in use: the result differs from the exact fp32 product
+    assert (y.detach().double().cpu() - b.detach().double().cpu() - xd.double() @ wd.double().T).abs().max() > 0
+
+
+def test_linear_bf16_gelu_on_load(mf):
+    torch.manual_seed(1)
+    h = torch.randn(257, 512, device=DEV)
+    w = torch.randn(192, 512, device=DEV) * 0.05
+    with mf.matmul_precision("bf16"):
+        y = mf.linear(h, w, None, in_gelu=True)
+    # GELU(h) is computed in fp32 on load and then rounded to bf16: a last-bit difference in
+    # the fp32 GELU can move an operand across a bf16 rounding boundary, so this one is held to
+    # the operand-rounding bound (two roundings of 2^-9 each) against the exact product
+    g = torch.nn.functional.gelu(h.double().cpu())
+    wc = w.cpu().double()
+    err = (y.double().cpu() - g @ wc.T).abs().max().item()
+    assert err <= 2.0 ** -8 * (g.abs() @ wc.abs().T).max().item(), err
+
+
+@pytest.mark.parametrize("cin,cout,k,pad,hw", [(64, 96, 3, 1, (17, 23)), (128, 64, 1, 0, (30, 40)),
+                                               (36, 48, 3, 1, (9, 12))])
+def test_conv_bf16_fwd_dgrad_wgrad(mf, cin, cout, k, pad, hw):
+    torch.manual_seed(2)
+    x = torch.randn(2, *hw, cin, device=DEV, requires_grad=True)  # NHWC
+    w = (torch.randn(cout, cin, k, k, device=DEV) * 0.1).requires_grad_()
+    with mf.matmul_precision("bf16"):
+        y = mf.conv2d_nhwc(x, w, None, stride=1, pad=pad)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+    xc = x.detach().cpu().permute(0, 3, 1, 2)
+    wc, dyc = w.detach().cpu(), dy.cpu().permute(0, 3, 1, 2)
+    conv = torch.nn.functional.conv2d
+    ref = conv(_r16(xc), _r16(wc), padding=pad)
+    absprod = conv(xc.double().abs(), wc.double().abs(), padding=pad)
+    _check_acc(y.permute(0, 3, 1, 2), ref, absprod, "conv fwd")
+    xr = _r16(xc).requires_grad_()
+    wr = _r16(wc).requires_grad_()
+    conv(xr, wr, padding=pad).backward(_r16(dyc))
+    xa = xc.double().abs().requires_grad_()
+    wa = wc.double().abs().requires_grad_()
+    conv(xa, wa, padding=pad).backward(dyc.double().abs())
+    _check_acc(x.grad.permute(0, 3, 1, 2), xr.grad, xa.grad, "conv dgrad")
+    _check_acc(w.grad, wr.grad, wa.grad, "conv wgrad")
+
+
+def test_depthformer_v8_decoder_bf16_vs_golden(mf):
+    """The golden decoder case (test_models_gpu.test_depthformer_v8_decoder_and_head) under bf16
+    matmuls against the reference's fp32 values.  Per tensor, the relative L2 error
+    ||got - ref|| / ||ref|| must stay within BF16_OUT_L2 (forward outputs) / BF16_GRAD_L2
+    (input and parameter gradients); the same case in fp32 sits at ~1e-6."""
+    import numpy as np
+
+    import test_models_gpu as tm
+    from mdemi.model.Depthformer import DepthformerV8
+    g = Golden("depthformer_v8")
+    holder = {}
+    m = DepthformerV8(tm.fake_backend(holder), tm.DFV8_OPT, min_depth=1e-3, max_depth=10.0)
+
+    def fwd(m, i):
+        holder.clear()
+        for k, v in i.items():
+            holder[int(k[1:])] = v
+        depth, centers, attn = m(torch.zeros(2, 3, 8, 8, device=DEV))
+        return (depth, centers) + tuple(attn)
+
+    errs, norms = {}, {}
+
+    def record(key, value, rtol, atol=0.0):
+        v = value.detach().double().cpu().numpy().reshape(-1)
+        if key in g.d:
+            ref = g.d[key].astype(np.float64).reshape(-1)
+        else:
+            v = v[::int(g.d["substep/" + key])]
+            ref = g.d["sub/" + key].astype(np.float64)
+        norms[key] = float(np.linalg.norm(ref) / np.sqrt(ref.size))
+        errs[key] = float(np.linalg.norm(v - ref) / (np.linalg.norm(ref) + 1e-30))
+
+    g.check = record
+    with mf.matmul_precision("bf16"):
+        n = tm.run_case(g, m, fwd, ["depth", "centers"] + [f"attn{k}" for k in range(8)], {},
+                        {k: "nchw" for k in g.input_names()})
+    assert n == len(list(m.parameters()))
+    # gradients that vanish in exact arithmetic (e.g. a key-projection bias: softmax is shift
+    # invariant) are rounding noise in fp32 and bf16 alike: they are held in absolute terms,
+    # ||got|| <= BF16_GRAD_L2 x the largest gradient norm, via the floor on the denominator
+    floor = max(norms[k] for k in norms if k.startswith("grad/")) * 1e-2
+    for k in errs:
+        if k.startswith("grad/") and norms[k] < floor:
+            errs[k] = errs[k] * norms[k] / floor
+    worst_out = max((e, k) for k, e in errs.items() if k.startswith("out/"))
+    worst_grad = max((e, k) for k, e in errs.items() if k.startswith("grad/"))
+    top = sorted(((e, k) for k, e in errs.items() if k.startswith("grad/")), reverse=True)[:5]
+    print(f"bf16 vs fp32 reference: worst output {worst_out}, worst gradients {top}")
+    assert worst_out[0] <= BF16_OUT_L2, worst_out
+    assert worst_grad[0] <= BF16_GRAD_L2, worst_grad
+
+
+def _dfv8_opt(drop):
+    return {"model": {"name": "depthformer_v8", "hidden_dim": 64, "num_heads": 4, "num_bins": 64, "num_aux": 32,
+                      "img_size": [128, 160], "bn_momentum": 0.1, "attn_drop_prob": drop, "drop_prob": drop},
+            "loss": {"alpha": 10.0, "beta": 0.5, "per_image": True, "chamfer_weight": 0.1},
+            "dataset": {"data_type": "NYU"}, "dataloader": {"batch_size": 2},
+            "optimizer": {"lr": 3.2e-4, "weight_decay": 0.1},
+            "scheduler": {"name": "onecycle", "pct_start": 0.15, "div_factor": 25, "final_div_factor": 100},
+            "train": {"epoch": 1, "num_accum": 1, "grad_norm": 0.1},
+            "eval": {"max_depth_eval": 10, "min_depth_eval": 0.001}}
+
+
+def _batch(seed):
+    g = torch.Generator().manual_seed(seed)
+    img = torch.randn(2, 3, 128, 160, generator=g)
+    gt = torch.rand(2, 1, 128, 160, generator=g) * 9.5 + 0.5
+    return img.to(DEV), gt.to(DEV)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_captured_step_matches_eager(mf, precision):
+    from mdemi.train import build_from_config
+    opt = _dfv8_opt(0.0)
+    torch.manual_seed(0)
+    eager = build_from_config(copy.deepcopy(opt), device=DEV, steps_per_epoch=20, precision=precision)
+    torch.manual_seed(0)
+    graph = build_from_config(copy.deepcopy(opt), device=DEV, steps_per_epoch=20, precision=precision, graph=True)
+    graph.model.load_state_dict(eager.model.state_dict())
+    batches = [_batch(s) for s in range(5)]
+    le, lg = [], []
+    for b in batches:  # graph: calls 1-2 run eagerly, 3 captures + replays, 4-5 replay
+        le.append(eager.step([b]).item())
+        lg.append(graph.step([b]).item())
+    assert graph._graph is not None
+    assert le == lg, (le, lg)
+    for (k, a), b in zip(eager.model.state_dict().items(), graph.model.state_dict().values()):
+        assert torch.equal(a, b), k
+    assert graph.optimizer.step_count == eager.optimizer.step_count == 5
+    assert int(graph.optimizer._step_dev.item()) == 5
+    for ge, gg in zip(eager.optimizer.param_groups, graph.optimizer.param_groups):
+        assert ge["lr"] == gg["lr"]
+
+
+def test_graph_replays_draw_new_dropout_masks(mf):
+    from mdemi.train import build_from_config
+    torch.manual_seed(0)
+    tr = build_from_config(_dfv8_opt(0.2), device=DEV, steps_per_epoch=20, precision="bf16", graph=True)
+    b = _batch(7)
+    losses = [tr.step([b]).item() for _ in range(5)]
+    assert all(torch.isfinite(torch.tensor(losses)))
+    # replays 3-5 see the same batch; dropout masks (and the weights) change between them
+    assert len(set(losses[2:])) == 3

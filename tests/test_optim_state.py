@@ -1,0 +1,63 @@
+"""FusedAdamW.state_dict / load_state_dict use torch.optim.AdamW's layout (state keyed by
+parameter position, per-parameter step, params index lists), so a state saved by either
+loads into the other, including a parameter whose gradient first appears after step 1
+(ADVICE r1).  CPU only: the state is built by hand, no kernel runs."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "monocular-depth-estimation_amd"))
+
+
+def _params():
+    torch.manual_seed(0)
+    return [torch.nn.Parameter(torch.randn(3, 2)), torch.nn.Parameter(torch.randn(4)),
+            torch.nn.Parameter(torch.randn(5))]
+
+
+def test_torch_adamw_state_loads_into_fused():
+    from mdemi.train import FusedAdamW
+    ps = _params()
+    ref = torch.optim.AdamW([{"params": ps[:2], "lr": 1e-3}, {"params": ps[2:], "lr": 1e-4}], weight_decay=0.1)
+    # step 1: only ps[1] and ps[2] have gradients; step 2: ps[0] too (it appears late)
+    ps[1].grad, ps[2].grad = torch.ones(4), torch.ones(5)
+    ref.step()
+    ps[0].grad = torch.ones(3, 2)
+    ref.step()
+    sd = ref.state_dict()
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    ours = FusedAdamW([{"params": qs[:2], "lr": 1e-3}, {"params": qs[2:], "lr": 1e-4}], weight_decay=0.1)
+    ours.load_state_dict(sd)
+    assert ours.step_count == 2
+    for p, q in zip(ps, qs):
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(ours.state[q][k], ref.state[p][k])
+    # and back into torch
+    sd2 = ours.state_dict()
+    assert sorted(sd2["state"]) == [0, 1, 2] and [g["params"] for g in sd2["param_groups"]] == [[0, 1], [2]]
+    ref2 = torch.optim.AdamW([{"params": ps[:2], "lr": 1e-3}, {"params": ps[2:], "lr": 1e-4}], weight_decay=0.1)
+    ref2.load_state_dict(sd2)
+    for p in ps:
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(ref2.state[p][k], ref.state[p][k])
+
+
+def test_state_keyed_by_position_not_first_gradient():
+    from mdemi.train import FusedAdamW
+    ps = _params()
+    opt = FusedAdamW(ps, lr=1e-3)
+    # state created in the order 2, 0 (gradient order), never for 1
+    for i in (2, 0):
+        opt.state[ps[i]] = {"exp_avg": torch.full_like(ps[i], float(i + 1)), "exp_avg_sq": torch.zeros_like(ps[i])}
+    opt.step_count = 3
+    sd = opt.state_dict()
+    assert sorted(sd["state"]) == [0, 2]
+    assert torch.equal(sd["state"][2]["exp_avg"], torch.full((5,), 3.0))
+    qs = _params()
+    opt2 = FusedAdamW(qs, lr=1e-3)
+    opt2.load_state_dict(sd)
+    assert qs[1] not in opt2.state
+    assert torch.equal(opt2.state[qs[2]]["exp_avg"], torch.full((5,), 3.0))
+    assert torch.equal(opt2.state[qs[0]]["exp_avg"], torch.full((3, 2), 1.0))
