@@ -39,6 +39,8 @@ import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (v_mfma_f32_32x32x2_f32)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense BF16 MFMA (no sparsity)
+# fp32e = fp32 GEMM as six bf16-plane products per 32x32x16 block: the bf16 MFMA peak / 6
+F32E_MFMA_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBS = 8000.0
 CPU_SHARE_PER_GPU = 16  # the GPU box's host-CPU share per GPU (OMP_NUM_THREADS there)
 
@@ -112,8 +114,10 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the KITTI 352x1216 secondary line")
-    ap.add_argument("--precision", default=None, choices=["fp32", "bf16"],
-                    help="matmul precision (default: the workload's; bf16 = bf16 operands, fp32 accumulate)")
+    ap.add_argument("--precision", default=None, choices=["fp32", "fp32e", "bf16"],
+                    help="matmul precision (default: the workload's). fp32: exact-product fp32 MFMA; fp32e: "
+                         "fp32 via three exact bf16 planes on the bf16 MFMA (fp32 error); bf16: bf16 operands, "
+                         "fp32 accumulate")
     ap.add_argument("--graph", action="store_true", help="capture the whole train step in a hipGraph")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: launcher/gloo plumbing check only (a toy model, not a measurement)")
@@ -235,10 +239,14 @@ def roofline_entry(trainer, batches, workload_key, ms):
     by, dom, tot_fl, tot_t = gemm_roofline(trainer, batches)
     (al, bl, aop, bop), (fl, t, cnt, alg) = dom
     ach = fl / t / 1e12
-    bf16 = trainer.precision == "bf16"
-    kname = "gemm_bf16_kernel" if bf16 else "gemm_f32_kernel"
-    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
-    regex = f"{kname}<{al}, {bl}, {aop}, {bop},"
+    prec = trainer.precision
+    if prec == "fp32":
+        kname, peak, regex = "gemm_f32_kernel", FP32_MFMA_PEAK_TFLOPS, f"gemm_f32_kernel<{al}, {bl}, {aop}, {bop},"
+    else:  # the 16-bit family: NP = 1 (bf16) or 3 (fp32e) planes
+        np_ = 1 if prec == "bf16" else 3
+        kname = "gemm_m16_kernel"
+        peak = BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else F32E_MFMA_PEAK_TFLOPS
+        regex = f"gemm_m16_kernel<{al}, {bl}, {aop}, {bop}, {np_},"
     traffic = profiled_traffic(regex, workload_key)
     alg_pl = alg / cnt
     roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
@@ -246,7 +254,7 @@ def roofline_entry(trainer, batches, workload_key, ms):
             "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
             "algorithmic_bytes": round(alg_pl), "traffic_over_algorithmic":
                 (round(traffic / alg_pl, 3) if traffic else None),
-            "kernel": f"{kname}<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}> (all pipelining variants)",
+            "kernel": f"{kname}<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}> ({prec}; all pipelining variants)",
             "kernel_regex": regex, "launches": cnt, "avg_launch_us": round(t / cnt * 1e6, 2),
             "flops_per_launch": fl / cnt}
     fams = {f"{KERNEL_NAME[k[0]]},{KERNEL_NAME[k[1]]},{k[2]},{k[3]}": {
@@ -492,7 +500,7 @@ def main():
     if key == "newcrfs" and not args.no_secondary and args.batch is None and args.height is None:
         wk = WORKLOADS["newcrfs_kitti"]
         sec = measure(args, wk["opt"], "newcrfs_kitti", wk["h"], wk["w"], 8, rank, world, device,
-                      with_roofline=not args.no_roofline)
+                      with_roofline=not args.no_roofline, precision=precision)
         del sec["trainer"]
         secondary = {"workload": wk["workload"], "reference_config": wk["ref_cfg"], "per_gpu_batch": 8,
                      "images_per_sec": round(sec["images"] / sec["elapsed"], 3), "ms_per_step": round(sec["ms"], 2),

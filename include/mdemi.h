@@ -121,11 +121,24 @@ int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream);
  * model/Depthformer/luna_layer.py:181-259, layer_utils.py:6-34) for the
  * mixed-precision train step.  Workspace: mdemi_gemm_workspace_size. */
 int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream);
+/* Same contract at fp32 accuracy on the bf16 matrix cores ("f32e"): each fp32
+ * operand is split exactly into three bf16 planes (a = a_hi + a_mid + a_lo, RNE)
+ * as it is staged and the six products hi.hi, hi.mid, mid.hi, hi.lo, lo.hi,
+ * mid.mid run on v_mfma_f32_32x32x16_bf16 with fp32 accumulation; the dropped
+ * terms are below 2^-26 |a||b|, under one fp32 rounding of a product, so results
+ * carry the error of mdemi_gemm_f32 (exact products, fp32 sums) at 2.67x its
+ * matrix-core peak.  Replaces the same fp32 nn.Linear / nn.Conv2d / bmm products
+ * as mdemi_gemm_f32 (swin_transformer.py:18-20,104,106,259; newcrf_layers.py:
+ * 16-20,102,104,384,389; uper_crf_head.py:38-44,341-348; ...). */
+int mdemi_gemm_f32e(const mdemi_gemm_desc* d, void* stream);
 /* tuning hook: pipelining variant (0..5, see gemm_f32.hip; -1 = time the
  * candidates once per distinct shape and cache the winner, the default -- all
  * variants produce bit-identical results) and tile raster (group_m > 0:
  * XCD-aware grouped raster, 0: plain).  Process-global. */
 int mdemi_gemm_set_variant(int32_t variant, int32_t group_m);
+/* tuning hook of the 16-bit family (mdemi_gemm_bf16 / mdemi_gemm_f32e): 0 = two
+ * LDS buffers, 1 = one, -1 = per-shape autotune (default; bit-identical). */
+int mdemi_gemm_set_variant_m16(int32_t variant);
 
 /* column / row sums (bias gradients: db[j] = sum_i dY[i][j])
  * replaces the bias-grad reduction autograd runs for every nn.Linear/Conv2d. */

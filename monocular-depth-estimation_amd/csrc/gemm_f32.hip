@@ -26,321 +26,13 @@
 // are remapped so that the tiles an XCD runs concurrently share A row-panels
 // and B column-panels in that XCD's L2 (guide T1).  Variants: see pick_variant.
 #include "common.h"
+#include "gemm_core.h"
 
 #include <map>
 #include <mutex>
 #include <tuple>
 
 namespace mdemi {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int GBM = 128, GBN = 128, GTHREADS = 256;
-constexpr int PMN = GBM + 4;   // [k][row] image pitch (floats)
-template <int BK> struct PitchK { static constexpr int v = BK + 4; };  // [row][k] image pitch
-
-struct FastDiv {
-  uint32_t mul, shift;
-};
-static inline FastDiv make_fastdiv(uint32_t d) {
-  uint32_t c = 0;
-  while ((1u << c) < d) ++c;
-  const uint32_t L = 31 + c;
-  return FastDiv{(uint32_t)(((uint64_t)1 << L) / d + 1), L};
-}
-
-struct GemmParams {
-  int M, N, K, batch, split, ktile_per_split;
-  const float* A; int64_t lda, a_bs;
-  const float* B; int64_t ldb, b_bs;
-  float* C; int64_t ldc, c_bs;
-  float alpha, beta;
-  const float* bias; int bias_mode, act;
-  const float* aux; int64_t ldaux, aux_bs;
-  const float* res; int64_t ldres, res_bs;
-  float* pre; int64_t ldpre, pre_bs;  // optional pre-activation output
-  float* rowsum;   // optional sum_k A(i,k) (A m-contiguous, batch 1): [split][M] partials or [M]
-  float* slab;  // split-K partials [split][batch][M][N]
-  mdemi_conv_geom cv;
-  FastDiv fd_c, fd_kw, fd_ow, fd_oh;  // conv index decomposition
-  int a_vec, b_vec;  // 1: 16-byte vector loads legal for this operand
-  int tiles_m, tiles_n, group_m;
-};
-
-// ---------------------------------------------------------------------------
-// Branch-free operand fetch.  Dense operands use buffer loads through a
-// wave-uniform descriptor rebased to the current K tile (SALU work only);
-// out-of-range elements get the offset BUF_OOB, which the hardware range check
-// turns into zeros.  NHWC gathers use 64-bit loads from a clamped address and
-// zero the result with a select.  No per-element control flow in the K loop.
-// ---------------------------------------------------------------------------
-constexpr int BUF_OOB = (int)0x80000000u;
-constexpr int BUF_RECORDS = 0x7fffffff;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, BUF_RECORDS, 0x00020000);
-}
-__device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-  return *reinterpret_cast<float4*>(&v);
-}
-__device__ __forceinline__ float buf_ld1(__amdgpu_buffer_rsrc_t r, int off) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-
-// n / d for 0 <= n < 2^31 by multiply-shift (host-computed magic, exact).
-__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
-  return (int)(((uint64_t)(uint32_t)n * f.mul) >> f.shift);
-}
-
-template <int OP>
-__device__ __forceinline__ float4 apply_op(float4 v) {
-  if (OP == MDEMI_OP_GELU) { v.x = gelu_f(v.x); v.y = gelu_f(v.y); v.z = gelu_f(v.z); v.w = gelu_f(v.w); }
-  return v;
-}
-
-// staged-image kinds
-constexpr int IMG_RK = 0;  // [row][k], pitch PK
-constexpr int IMG_KR = 1;  // [k][row], pitch PMN (written as float4 rows)
-constexpr int IMG_KT = 2;  // [k][row], pitch GBM+2, written transposed (4x ds_write_b32) from a row-major source
-
-template <int IMG, int BK>
-struct Img {
-  static constexpr int PK = PitchK<BK>::v;
-  static constexpr int PT = (IMG == IMG_KT) ? GBM + 2 : PMN;
-  static constexpr int floats = (IMG == IMG_RK) ? GBM * PK : BK * PT;
-  // 4 consecutive MFMA k-steps (group t) for fragment row `r` of this lane half h
-  __device__ static float4 frag(const float* s, int r, int t, int h) {
-    if (IMG == IMG_RK) return *reinterpret_cast<const float4*>(s + r * PK + 8 * t + 4 * h);
-    const float* p = s + (8 * t + 4 * h) * PT + r;
-    return make_float4(p[0], p[PT], p[2 * PT], p[3 * PT]);
-  }
-};
-
-// ---------------------------------------------------------------------------
-// Operand loaders: each thread stages NQ = BK/8 float4 per operand per K tile.
-//   row-major tile  (128 rows x BK k): f = t + 256 q -> row f/(BK/4), k-quad f%(BK/4)
-//   k-major tile    (BK k x 128 cols): f = t + 256 q -> k f>>5, col-quad f&31
-// ---------------------------------------------------------------------------
-template <int BK>
-__device__ __forceinline__ void store_rk(float* lds, int t, const float4 (&r)[BK / 8]) {
-  constexpr int KQ = BK / 4, RS = 256 / KQ;
-#pragma unroll
-  for (int q = 0; q < BK / 8; ++q)
-    *reinterpret_cast<float4*>(lds + (t / KQ + RS * q) * PitchK<BK>::v + 4 * (t % KQ)) = r[q];
-}
-// row-major source tile transposed into a [k][row] image (pitch 130: the 4
-// k-rows a 32-lane group writes land on distinct banks)
-template <int BK>
-__device__ __forceinline__ void store_kt(float* lds, int t, const float4 (&r)[BK / 8]) {
-  constexpr int KQ = BK / 4, RS = 256 / KQ, P = GBM + 2;
-#pragma unroll
-  for (int q = 0; q < BK / 8; ++q) {
-    const int row = t / KQ + RS * q, k = 4 * (t % KQ);
-    lds[(k + 0) * P + row] = r[q].x;
-    lds[(k + 1) * P + row] = r[q].y;
-    lds[(k + 2) * P + row] = r[q].z;
-    lds[(k + 3) * P + row] = r[q].w;
-  }
-}
-template <int BK>
-__device__ __forceinline__ void store_kr(float* lds, int t, const float4 (&r)[BK / 8]) {
-#pragma unroll
-  for (int q = 0; q < BK / 8; ++q)
-    *reinterpret_cast<float4*>(lds + ((t >> 5) + 8 * q) * PMN + 4 * (t & 31)) = r[q];
-}
-
-template <int LAYOUT, int OP, bool IS_A, int BK, bool TR>
-struct Loader;
-
-// dense [row][k]: thread t covers rows t/KQ + RS*q, k-quad t%KQ
-template <int OP, bool IS_A, int BK, bool TR>
-struct Loader<MDEMI_L_KCONTIG, OP, IS_A, BK, TR> {
-  static constexpr int IMG = TR ? IMG_KT : IMG_RK, NQ = BK / 8, KQ = BK / 4, RS = 256 / KQ;
-  const float* base; int K; bool vec;
-  int voff[NQ]; int kq;
-  __device__ void init(const float* p, int64_t ld, int rows, int K_, bool vec_, int r0, int t, const GemmParams&) {
-    base = p + (int64_t)r0 * ld; K = K_; vec = vec_; kq = t % KQ;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int row = t / KQ + RS * q;
-      voff[q] = r0 + row < rows ? (int)(((int64_t)row * ld + 4 * kq) * 4) : BUF_OOB;
-    }
-  }
-  __device__ void load(int k0, float4 (&r)[NQ]) const {
-    const auto rs = make_rsrc(base + k0);
-    const int k = k0 + 4 * kq;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      if (vec) {
-        r[q] = buf_ld4(rs, k < K ? voff[q] : BUF_OOB);
-      } else {
-        r[q].x = buf_ld1(rs, k + 0 < K ? voff[q] + 0 : BUF_OOB);
-        r[q].y = buf_ld1(rs, k + 1 < K ? voff[q] + 4 : BUF_OOB);
-        r[q].z = buf_ld1(rs, k + 2 < K ? voff[q] + 8 : BUF_OOB);
-        r[q].w = buf_ld1(rs, k + 3 < K ? voff[q] + 12 : BUF_OOB);
-      }
-      r[q] = apply_op<OP>(r[q]);
-    }
-  }
-  __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) {
-    if (TR) store_kt<BK>(lds, t, r); else store_rk<BK>(lds, t, r);
-  }
-};
-
-// dense [k][row]: thread t covers k rows t/32 + 8q, column quad t%32
-template <int OP, bool IS_A, int BK, bool TR>
-struct Loader<MDEMI_L_MNCONTIG, OP, IS_A, BK, TR> {
-  static constexpr int IMG = IMG_KR, NQ = BK / 8;
-  const float* base; int64_t ld; int K; bool vec;
-  int voff; int kl; int cvalid;  // valid columns of this thread's quad (0..4)
-  __device__ void init(const float* p, int64_t ld_, int cols, int K_, bool vec_, int c0, int t, const GemmParams&) {
-    base = p + c0; ld = ld_; K = K_; vec = vec_;
-    const int col = 4 * (t & 31);
-    kl = t >> 5;
-    cvalid = max(0, min(4, cols - c0 - col));
-    voff = (int)(((int64_t)kl * ld + col) * 4);
-  }
-  __device__ void load(int k0, float4 (&r)[NQ]) const {
-    const auto rs = make_rsrc(base + (int64_t)k0 * ld);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const bool kin = k0 + kl + 8 * q < K;
-      const int off = voff + (int)(8 * q * ld * 4);
-      if (vec) {
-        r[q] = buf_ld4(rs, kin && cvalid > 0 ? off : BUF_OOB);
-      } else {
-        r[q].x = buf_ld1(rs, kin && cvalid > 0 ? off + 0 : BUF_OOB);
-        r[q].y = buf_ld1(rs, kin && cvalid > 1 ? off + 4 : BUF_OOB);
-        r[q].z = buf_ld1(rs, kin && cvalid > 2 ? off + 8 : BUF_OOB);
-        r[q].w = buf_ld1(rs, kin && cvalid > 3 ? off + 12 : BUF_OOB);
-      }
-      r[q] = apply_op<OP>(r[q]);
-    }
-  }
-  __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) { store_kr<BK>(lds, t, r); }
-};
-
-__device__ __forceinline__ float4 gather4(const float* base, int64_t idx, bool ok) {
-  const float4 v = *reinterpret_cast<const float4*>(base + (ok ? idx : 0));
-  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-// Implicit im2col of an NHWC activation, operand A (row = output pixel,
-// k = (ky,kx,c)).  Requires C % 4 == 0 so a k-quad never straddles a tap.
-template <int OP, int BK, bool TR>
-struct Loader<MDEMI_L_CONV, OP, true, BK, TR> {
-  static constexpr int IMG = TR ? IMG_KT : IMG_RK, NQ = BK / 8, KQ = BK / 4, RS = 256 / KQ;
-  const float* base; mdemi_conv_geom g; FastDiv fc, fkw; int K; int kq;
-  int n[NQ], iy0[NQ], ix0[NQ]; bool valid[NQ];
-  __device__ void init(const float* p, int64_t, int rows, int K_, bool, int r0, int t, const GemmParams& P) {
-    base = p; g = P.cv; fc = P.fd_c; fkw = P.fd_kw; K = K_; kq = t % KQ;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int i = r0 + t / KQ + RS * q;
-      valid[q] = i < rows;
-      const int ii = valid[q] ? i : 0;
-      const int tmp = fdiv(ii, P.fd_ow), ox = ii - tmp * g.ow;
-      const int nn = fdiv(tmp, P.fd_oh), oy = tmp - nn * g.oh;
-      n[q] = nn;
-      iy0[q] = oy * g.stride - g.pad;
-      ix0[q] = ox * g.stride - g.pad;
-    }
-  }
-  __device__ void load(int k0, float4 (&r)[NQ]) const {
-    const int k = k0 + 4 * kq;
-    const bool kin = k < K;
-    const int kk = kin ? k : 0;
-    const int tap = fdiv(kk, fc), c = kk - tap * g.c;
-    const int ky = fdiv(tap, fkw), kx = tap - ky * g.kw;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      int iy = iy0[q] + ky, ix = ix0[q] + kx;
-      bool ok = kin && valid[q];
-      if (g.pad_mode == MDEMI_PAD_REPLICATE) {
-        iy = min(max(iy, 0), g.h - 1); ix = min(max(ix, 0), g.w - 1);
-      } else {
-        ok = ok && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
-      }
-      r[q] = apply_op<OP>(gather4(base, (((int64_t)n[q] * g.h + iy) * g.w + ix) * g.c + c, ok));
-    }
-  }
-  __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) {
-    if (TR) store_kt<BK>(lds, t, r); else store_rk<BK>(lds, t, r);
-  }
-};
-
-// Implicit im2col, operand B (weight gradients): B(k, j) with k = output pixel,
-// j = (ky,kx,c); staged k-major like a dense [k][col] operand.
-template <int OP, int BK, bool TR>
-struct Loader<MDEMI_L_CONV, OP, false, BK, TR> {
-  static constexpr int IMG = IMG_KR, NQ = BK / 8;
-  const float* base; mdemi_conv_geom g; FastDiv fow, foh; int K; int kl;
-  int c, ky, kx; bool jvalid;
-  __device__ void init(const float* p, int64_t, int cols, int K_, bool, int c0, int t, const GemmParams& P) {
-    base = p; g = P.cv; fow = P.fd_ow; foh = P.fd_oh; K = K_; kl = t >> 5;
-    const int j = c0 + 4 * (t & 31);
-    jvalid = j < cols;
-    const int jj = jvalid ? j : 0;
-    const int tap = fdiv(jj, P.fd_c);
-    c = jj - tap * g.c;
-    ky = fdiv(tap, P.fd_kw);
-    kx = tap - ky * g.kw;
-  }
-  __device__ void load(int k0, float4 (&r)[NQ]) const {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int k = k0 + kl + 8 * q;
-      bool ok = jvalid && k < K;
-      const int kk = ok ? k : 0;
-      const int tmp = fdiv(kk, fow), ox = kk - tmp * g.ow;
-      const int nn = fdiv(tmp, foh), oy = tmp - nn * g.oh;
-      int iy = oy * g.stride - g.pad + ky, ix = ox * g.stride - g.pad + kx;
-      if (g.pad_mode == MDEMI_PAD_REPLICATE) {
-        iy = min(max(iy, 0), g.h - 1); ix = min(max(ix, 0), g.w - 1);
-      } else {
-        ok = ok && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
-      }
-      r[q] = apply_op<OP>(gather4(base, (((int64_t)nn * g.h + iy) * g.w + ix) * g.c + c, ok));
-    }
-  }
-  __device__ static void store(float* lds, int t, const float4 (&r)[NQ]) { store_kr<BK>(lds, t, r); }
-};
-
-
-__device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int i, int j, float acc) {
-  float v = p.alpha * acc;
-  if (p.beta != 0.f) v += p.beta * p.C[(int64_t)b * p.c_bs + (int64_t)i * p.ldc + j];
-  if (p.bias_mode == MDEMI_BIAS_COL) v += p.bias[j];
-  else if (p.bias_mode == MDEMI_BIAS_ROW) v += p.bias[i];
-  if (p.pre) p.pre[(int64_t)b * p.pre_bs + (int64_t)i * p.ldpre + j] = v;
-  if (is_grad_act(p.act)) v *= aux_grad(p.act, p.aux[(int64_t)b * p.aux_bs + (int64_t)i * p.ldaux + j]);
-  else if (p.act != MDEMI_ACT_NONE) v = apply_act(p.act, v);
-  if (p.res) v += p.res[(int64_t)b * p.res_bs + (int64_t)i * p.ldres + j];
-  return v;
-}
-
-// tile (tm, tn) for a linear workgroup id: XCD-aware remap (blocks b, b+8, ...
-// share an XCD), then grouped raster so concurrently running tiles of one XCD
-// reuse A row-panels (group_m rows of tiles) and B column-panels.
-__device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles, int& tm, int& tn) {
-  if (p.group_m <= 0) {  // plain raster: n fastest
-    tm = bid / p.tiles_n;
-    tn = bid % p.tiles_n;
-    return;
-  }
-  const int q = ntiles / 8, r = ntiles % 8;
-  const int xcd = bid % 8, idx = bid / 8;
-  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  const int per_group = p.group_m * p.tiles_n;
-  const int grp = lin / per_group;
-  const int first_m = grp * p.group_m;
-  const int gm = min(p.tiles_m - first_m, p.group_m);
-  const int in_grp = lin % per_group;
-  tm = first_m + in_grp % gm;
-  tn = in_grp / gm;
-}
-
 
 // Pipelining variants (A/B-tested on the model's shapes, tools/gemm_bench.py):
 //   BK    K depth per LDS tile (16 or 32)
@@ -477,157 +169,6 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 #include "gemm_epilogue.inc"
 }
 
-// ---------------------------------------------------------------------------
-// bf16-compute variant (mixed precision, BASELINE configs[4]): the same
-// operand loaders fetch fp32 from HBM, values are rounded to bf16 (RNE,
-// v_cvt_pk_bf16_f32) on their way into LDS, products run on
-// v_mfma_f32_32x32x16_bf16 (16x the fp32 MFMA rate) with fp32 accumulation,
-// and the fp32 epilogue is shared with the fp32 kernel.  This is autocast's
-// numerics (bf16 operands, fp32 accumulate) with an fp32 result.
-//
-// LDS images are [row][k] bf16 for both operands (B as [col][k]), pitch
-// BK + 8 elements: a lane's MFMA fragment (8 consecutive k of one row) is one
-// conflict-free ds_read_b128.  k-contiguous sources (row-major A, [N][K]
-// weights, NHWC im2col rows) store 4 bf16 per float4 with one ds_write_b64;
-// m/n-contiguous sources scatter 4 ds_write_b16 per float4.
-// MFMA 32x32x16 lane maps: lane l (r = l&31, h = l>>5) holds A[r][8h + j] and
-// B[8h + j][r], j = 0..7, for the 16-deep k-step.
-// ---------------------------------------------------------------------------
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-
-template <int IMG, int BK>
-__device__ __forceinline__ void store_bf16(__bf16* img, int t, const float4 (&r)[BK / 8]) {
-  constexpr int PB = BK + 8, NQ = BK / 8;
-  if constexpr (IMG == IMG_KR) {  // float4 runs along rows/cols at one k: k = t/32 + 8q, cols 4*(t&31) + i
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      __bf16* d = img + (4 * (t & 31)) * PB + (t >> 5) + 8 * q;
-      d[0] = (__bf16)r[q].x;
-      d[PB] = (__bf16)r[q].y;
-      d[2 * PB] = (__bf16)r[q].z;
-      d[3 * PB] = (__bf16)r[q].w;
-    }
-  } else {  // float4 runs along k: row t/KQ + RS*q, k 4*(t%KQ)
-    constexpr int KQ = BK / 4, RS = 256 / KQ;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      bf16x4_t v;
-      v[0] = (__bf16)r[q].x; v[1] = (__bf16)r[q].y; v[2] = (__bf16)r[q].z; v[3] = (__bf16)r[q].w;
-      *reinterpret_cast<bf16x4_t*>(img + (t / KQ + RS * q) * PB + 4 * (t % KQ)) = v;
-    }
-  }
-}
-
-template <int AL, int BL, int AOP, int BOP, int BK, int OCC>
-__global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void gemm_bf16_kernel(GemmParams p) {
-  using LA = Loader<AL, AOP, true, BK, false>;
-  using LB = Loader<BL, BOP, false, BK, false>;
-  constexpr int NQ = BK / 8, PB = BK + 8, IMGE = GBM * PB;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * IMGE];
-
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int ntiles = p.tiles_m * p.tiles_n;
-  const int zb = blockIdx.x / ntiles;
-  int tm, tn;
-  tile_of(p, blockIdx.x % ntiles, ntiles, tm, tn);
-  const int b = zb / p.split, sidx = zb % p.split;
-  const int bm = tm * GBM, bn = tn * GBN;
-
-  LA la;
-  LB lb;
-  la.init(p.A + (int64_t)b * p.a_bs, p.lda, p.M, p.K, p.a_vec, bm, t, p);
-  lb.init(p.B + (int64_t)b * p.b_bs, p.ldb, p.N, p.K, p.b_vec, bn, t, p);
-
-  const int ktiles_total = (p.K + BK - 1) / BK;
-  const int kt_begin = sidx * p.ktile_per_split;
-  const int kt_end = min(ktiles_total, kt_begin + p.ktile_per_split);
-
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
-
-  float4 ra[NQ], rb[NQ];
-  constexpr bool CAN_RSUM = AL == MDEMI_L_MNCONTIG;
-  const bool do_rsum = CAN_RSUM && p.rowsum != nullptr && tn == 0;
-  float4 rsum = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto acc_rsum = [&]() {  // fp32 row sums of the unrounded A (bias gradient)
-    if (CAN_RSUM && do_rsum) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        rsum.x += ra[q].x; rsum.y += ra[q].y; rsum.z += ra[q].z; rsum.w += ra[q].w;
-      }
-    }
-  };
-  const int l31 = lane & 31, h = lane >> 5;
-  const int ra0 = wm * 64 + l31, ra1 = ra0 + 32;
-  const int rb0 = wn * 64 + l31, rb1 = rb0 + 32;
-
-  if (kt_begin < kt_end) {
-    la.load(kt_begin * BK, ra);
-    lb.load(kt_begin * BK, rb);
-    store_bf16<LA::IMG, BK>(smem, t, ra);
-    store_bf16<LB::IMG, BK>(smem + IMGE, t, rb);
-    acc_rsum();
-    __syncthreads();
-  }
-  int cur = 0;
-  for (int kt = kt_begin; kt < kt_end; ++kt) {
-    const bool more = kt + 1 < kt_end;
-    if (more) {  // issue the next tile's loads early; they land under the MFMAs
-      la.load((kt + 1) * BK, ra);
-      lb.load((kt + 1) * BK, rb);
-    }
-    const __bf16* a_s = smem + cur * 2 * IMGE;
-    const __bf16* b_s = a_s + IMGE;
-#pragma unroll
-    for (int kk = 0; kk < BK / 16; ++kk) {
-      const int ko = 16 * kk + 8 * h;
-      const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(a_s + ra0 * PB + ko);
-      const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(a_s + ra1 * PB + ko);
-      const bf16x8_t b0 = *reinterpret_cast<const bf16x8_t*>(b_s + rb0 * PB + ko);
-      const bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(b_s + rb1 * PB + ko);
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (more) {
-      __bf16* dst = smem + (cur ^ 1) * 2 * IMGE;
-      store_bf16<LA::IMG, BK>(dst, t, ra);
-      store_bf16<LB::IMG, BK>(dst + IMGE, t, rb);
-      acc_rsum();
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
-  if (CAN_RSUM && do_rsum) {  // reduce the 8 k-row groups (t >> 5) through LDS
-    float4* red = reinterpret_cast<float4*>(smem);
-    red[t] = rsum;
-    __syncthreads();
-    if (t < 32) {
-      float4 s4 = red[t];
-#pragma unroll
-      for (int g = 1; g < 8; ++g) {
-        const float4 o = red[t + 32 * g];
-        s4.x += o.x; s4.y += o.y; s4.z += o.z; s4.w += o.w;
-      }
-      float* dst = p.rowsum + (p.split > 1 ? (int64_t)sidx * p.M : 0);
-      const int i = bm + 4 * t;
-      if (i + 0 < p.M) dst[i + 0] = s4.x;
-      if (i + 1 < p.M) dst[i + 1] = s4.y;
-      if (i + 2 < p.M) dst[i + 2] = s4.z;
-      if (i + 3 < p.M) dst[i + 3] = s4.w;
-    }
-  }
-#include "gemm_epilogue.inc"
-}
-
 // Deterministic split-K combine + epilogue: sums slabs in split order.
 // Deterministic split-K combine + epilogue: sums slabs in split order, four
 // consecutive columns per thread when N % 4 == 0; also folds the row-sum
@@ -688,7 +229,7 @@ using KernelFn = void (*)(GemmParams);
 // boundaries, so the choice never changes a result bit.
 constexpr int NVARIANTS = 6;
 static int g_variant = -1;  // -1: autotune per shape
-static int g_variant_bf16 = -1;
+static int g_variant_m16 = -1;  // 16-bit family (bf16 / split fp32): 0 two LDS buffers, 1 one
 static int g_group_m = 8;
 
 template <int AL, int BL, int AOP, int BOP>
@@ -730,39 +271,7 @@ static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
   return nullptr;
 }
 
-// bf16-compute family: variant 0 = BK 32 (2 workgroups/CU by LDS), 1 = BK 64.
-template <int AL, int BL, int AOP, int BOP>
-static KernelFn pick_variant_bf16(int v) {
-  if (v == 1) return gemm_bf16_kernel<AL, BL, AOP, BOP, 64, 1>;
-  return gemm_bf16_kernel<AL, BL, AOP, BOP, 32, 2>;
-}
-template <int AL, int BL>
-static KernelFn pick_ops_bf16(int aop, int bop, int v) {
-  if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_NONE) return pick_variant_bf16<AL, BL, MDEMI_OP_NONE, MDEMI_OP_NONE>(v);
-  if constexpr (AL == MDEMI_L_KCONTIG)
-    if (aop == MDEMI_OP_GELU && bop == MDEMI_OP_NONE)
-      return pick_variant_bf16<AL, BL, MDEMI_OP_GELU, MDEMI_OP_NONE>(v);
-  if constexpr (BL == MDEMI_L_MNCONTIG)
-    if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_GELU)
-      return pick_variant_bf16<AL, BL, MDEMI_OP_NONE, MDEMI_OP_GELU>(v);
-  return nullptr;
-}
-static KernelFn pick_kernel_bf16(int al, int bl, int aop, int bop, int v) {
-#define MDEMI_PICK(X, Y) \
-  if (al == X && bl == Y) return pick_ops_bf16<X, Y>(aop, bop, v);
-  MDEMI_PICK(MDEMI_L_KCONTIG, MDEMI_L_KCONTIG)
-  MDEMI_PICK(MDEMI_L_KCONTIG, MDEMI_L_MNCONTIG)
-  MDEMI_PICK(MDEMI_L_MNCONTIG, MDEMI_L_KCONTIG)
-  MDEMI_PICK(MDEMI_L_MNCONTIG, MDEMI_L_MNCONTIG)
-  MDEMI_PICK(MDEMI_L_CONV, MDEMI_L_KCONTIG)
-  MDEMI_PICK(MDEMI_L_CONV, MDEMI_L_MNCONTIG)
-  MDEMI_PICK(MDEMI_L_MNCONTIG, MDEMI_L_CONV)
-  MDEMI_PICK(MDEMI_L_KCONTIG, MDEMI_L_CONV)
-#undef MDEMI_PICK
-  return nullptr;
-}
-
-static int variant_bk(int v, bool bf16) { return bf16 ? (v == 1 ? 64 : 32) : (v >= 3 ? 32 : 16); }
+static int variant_bk(int v, int mode) { return mode != GEMM_F32 ? 32 : (v >= 3 ? 32 : 16); }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -801,8 +310,8 @@ static int validate(const mdemi_gemm_desc* d) {
   return MDEMI_OK;
 }
 
-static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, bool bf16) {
-  const int GBK = variant_bk(variant, bf16);
+static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, int mode) {
+  const int GBK = variant_bk(variant, mode);
   p.M = d->M; p.N = d->N; p.K = d->K; p.batch = d->batch;
   p.A = d->A; p.lda = d->lda; p.a_bs = d->a_bstride;
   p.B = d->B; p.ldb = d->ldb; p.b_bs = d->b_bstride;
@@ -814,9 +323,9 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, bo
   p.cv = d->conv;
   p.pre = d->preact; p.ldpre = d->ldpre; p.pre_bs = d->pre_bstride;
   p.rowsum = d->rowsum_a;
-  // split boundaries in fixed K chunks whatever the variant's BK (32 elements for the
-  // fp32 family, 64 for bf16), so the variants of a family agree bit for bit
-  const int CH = bf16 ? 64 : 32;
+  // split boundaries in fixed 32-element K chunks whatever the variant's BK, so the
+  // variants of a family agree bit for bit
+  const int CH = 32;
   const int kc = (int)cdiv(d->K, CH);
   const int split = d->split_k < kc ? d->split_k : kc;
   const int chunks_per_split = (int)cdiv(kc, split);
@@ -859,16 +368,17 @@ static size_t colsum_combine_bytes(const mdemi_gemm_desc* d, const GemmParams& p
   return colsum_combine(d, p) ? colsum_ws_bytes(p.split, (int64_t)d->M * d->N) : 0;
 }
 
-static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, bool bf16) {
-  KernelFn fn = bf16 ? pick_kernel_bf16(d->a_layout, d->b_layout, d->a_op, d->b_op, variant)
-                     : pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant);
+static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mode) {
+  KernelFn fn = mode == GEMM_F32 ? pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant)
+                                 : pick_kernel_m16(d->a_layout, d->b_layout, d->a_op, d->b_op,
+                                                   mode == GEMM_BF16 ? 1 : 3, variant);
   if (!fn) {
     set_error("gemm: unsupported layout/op combination a=%d/%d b=%d/%d", d->a_layout, d->a_op, d->b_layout,
               d->b_op);
     return MDEMI_EUNSUP;
   }
   GemmParams p;
-  fill_params(d, p, variant, bf16);
+  fill_params(d, p, variant, mode);
   float* rowsum_part = nullptr;
   if (p.split > 1) {
     const size_t need = slab_bytes(d, p) + rowsum_bytes(d, p) + colsum_combine_bytes(d, p);
@@ -901,14 +411,14 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, bool bf
                          rowsum_part ? d->rowsum_a : (float*)nullptr);
     }
   }
-  return check_launch(bf16 ? "gemm_bf16" : "gemm_f32");
+  return check_launch(mode == GEMM_BF16 ? "gemm_bf16" : mode == GEMM_F32E ? "gemm_f32e" : "gemm_f32");
 }
 
 struct TuneKey {
-  int al, bl, aop, bop, M, N, K, batch, split, bf16;
+  int al, bl, aop, bop, M, N, K, batch, split, mode;
   bool operator<(const TuneKey& o) const {
-    return std::tie(al, bl, aop, bop, M, N, K, batch, split, bf16) <
-           std::tie(o.al, o.bl, o.aop, o.bop, o.M, o.N, o.K, o.batch, o.split, o.bf16);
+    return std::tie(al, bl, aop, bop, M, N, K, batch, split, mode) <
+           std::tie(o.al, o.bl, o.aop, o.bop, o.M, o.N, o.K, o.batch, o.split, o.mode);
   }
 };
 static std::map<TuneKey, int> g_tuned;
@@ -925,9 +435,9 @@ static bool tunable(const mdemi_gemm_desc* d, hipStream_t st) {
   return true;
 }
 
-static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, bool bf16) {
-  if (bf16 ? g_variant_bf16 >= 0 : g_variant >= 0) return bf16 ? g_variant_bf16 : g_variant;
-  const TuneKey key{d->a_layout, d->b_layout, d->a_op, d->b_op, d->M, d->N, d->K, d->batch, d->split_k, (int)bf16};
+static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
+  if (mode != GEMM_F32 ? g_variant_m16 >= 0 : g_variant >= 0) return mode != GEMM_F32 ? g_variant_m16 : g_variant;
+  const TuneKey key{d->a_layout, d->b_layout, d->a_op, d->b_op, d->M, d->N, d->K, d->batch, d->split_k, mode};
   {
     std::lock_guard<std::mutex> lk(g_tune_mu);
     auto it = g_tuned.find(key);
@@ -935,18 +445,18 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, bool bf16) {
   }
   if (!tunable(d, st)) return 0;
   static const int cands_f32[] = {0, 1, 3, 4, 5};
-  static const int cands_bf16[] = {0, 1};
-  const int* cands = bf16 ? cands_bf16 : cands_f32;
-  const int ncand = bf16 ? 2 : 5;
+  static const int cands_m16[] = {0, 1};
+  const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
+  const int ncand = mode != GEMM_F32 ? 2 : 5;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 0;
   int best = 0;
   float best_ms = 1e30f;
   for (int ci = 0; ci < ncand; ++ci) {
     const int v = cands[ci];
-    if (launch(d, v, st, bf16) != MDEMI_OK) continue;  // warm (and validate)
+    if (launch(d, v, st, mode) != MDEMI_OK) continue;  // warm (and validate)
     (void)hipEventRecord(e0, st);
-    for (int r = 0; r < 3; ++r) launch(d, v, st, bf16);
+    for (int r = 0; r < 3; ++r) launch(d, v, st, mode);
     (void)hipEventRecord(e1, st);
     float ms = 0.f;
     if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
@@ -962,35 +472,35 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, bool bf16) {
 extern "C" size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d) {
   if (!d || d->split_k <= 1) return 0;
   GemmParams p;
-  fill_params(d, p, 0, false);  // the split count does not depend on the variant
-  GemmParams pb;
-  fill_params(d, pb, 0, true);  // bf16 family: 64-element split chunks (never more splits)
-  if (p.split <= 1 && pb.split <= 1) return 0;
-  if (pb.split > p.split) p = pb;
+  fill_params(d, p, 0, GEMM_F32);  // every family splits at the same 32-element chunks
   if (p.split <= 1) return 0;
   return slab_bytes(d, p) + rowsum_bytes(d, p) + colsum_combine_bytes(d, p);
 }
 
-extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) {
+static int gemm_entry(const mdemi_gemm_desc* d, void* stream, int mode) {
   int rc = validate(d);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  return launch(d, choose_variant(d, st, false), st, false);
+  return launch(d, choose_variant(d, st, mode), st, mode);
 }
 
-extern "C" int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream) {
-  int rc = validate(d);
-  if (rc) return rc;
-  hipStream_t st = (hipStream_t)stream;
-  return launch(d, choose_variant(d, st, true), st, true);
-}
+extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) { return gemm_entry(d, stream, GEMM_F32); }
+extern "C" int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream) { return gemm_entry(d, stream, GEMM_BF16); }
+extern "C" int mdemi_gemm_f32e(const mdemi_gemm_desc* d, void* stream) { return gemm_entry(d, stream, GEMM_F32E); }
 
-// Benchmark/tuning hook: force a pipelining variant (see pick_variant; -1 =
-// per-shape autotune, the default) and the tile raster (group_m > 0:
-// XCD-aware grouped raster; 0: plain).
+// Benchmark/tuning hook: force a pipelining variant of the fp32 family (see
+// pick_variant) and of the 16-bit family (0: two LDS buffers, 1: one; -1 =
+// per-shape autotune, the default) and the tile raster (group_m > 0: XCD-aware
+// grouped raster; 0: plain).
 extern "C" int mdemi_gemm_set_variant(int32_t variant, int32_t group_m) {
   MDEMI_REQUIRE(variant >= -1 && variant < NVARIANTS && group_m >= 0, "gemm_set_variant: bad args");
   g_variant = variant;
   g_group_m = group_m;
+  return MDEMI_OK;
+}
+
+extern "C" int mdemi_gemm_set_variant_m16(int32_t variant) {
+  MDEMI_REQUIRE(variant >= -1 && variant < 2, "gemm_set_variant_m16: bad variant");
+  g_variant_m16 = variant;
   return MDEMI_OK;
 }

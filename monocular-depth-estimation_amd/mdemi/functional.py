@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -61,15 +62,23 @@ def _drop(src_ptr, dst_ptr, n, p, seed, add=0, offset=0):
     L.call("mdemi_dropout_dev", src_ptr, dst_ptr, n, float(p), seed.data_ptr(), add, offset, L.stream())
 
 
-# Matmul precision of every libmdemi GEMM: "fp32" (exact fp32 MFMA, the reference's
-# precision) or "bf16" (bf16 operands, fp32 accumulate: torch.autocast's matmul numerics,
-# BASELINE configs[4]).  Process-wide; set it for a whole train step (forward and backward).
-_PRECISION = ["fp32"]
+# Matmul precision of every libmdemi GEMM:
+#   "fp32"  exact-product fp32 MFMA (v_mfma_f32_32x32x2_f32), the reference's precision;
+#   "fp32e" fp32 on the bf16 matrix cores: operands split exactly into three bf16 planes,
+#           six plane products, fp32 accumulation -- the error of "fp32" (dropped terms
+#           < 2^-26 |a||b|) at 2.67x its peak (mdemi_gemm_f32e);
+#   "bf16"  bf16 operands, fp32 accumulate: torch.autocast's matmul numerics (BASELINE
+#           configs[4]).
+# Process-wide; set it for a whole train step (forward and backward).
+PRECISIONS = ("fp32", "fp32e", "bf16")
+_PRECISION = [os.environ.get("MDEMI_MATMUL_PRECISION", "fp32")]
+if _PRECISION[0] not in PRECISIONS:
+    raise ValueError(f"MDEMI_MATMUL_PRECISION must be one of {PRECISIONS}, got {_PRECISION[0]!r}")
 
 
 def set_matmul_precision(precision: str) -> None:
-    if precision not in ("fp32", "bf16"):
-        raise ValueError(f"matmul precision must be 'fp32' or 'bf16', got {precision!r}")
+    if precision not in PRECISIONS:
+        raise ValueError(f"matmul precision must be one of {PRECISIONS}, got {precision!r}")
     _PRECISION[0] = precision
 
 
@@ -122,6 +131,8 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     if _PRECISION[0] == "bf16":
         L.check(lib.mdemi_gemm_bf16(ctypes.byref(d), L.stream()), "gemm_bf16")
+    elif _PRECISION[0] == "fp32e":
+        L.check(lib.mdemi_gemm_f32e(ctypes.byref(d), L.stream()), "gemm_f32e")
     else:
         L.check(lib.mdemi_gemm_f32(ctypes.byref(d), L.stream()), "gemm_f32")
     return C

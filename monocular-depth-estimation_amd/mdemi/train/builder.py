@@ -161,8 +161,9 @@ class Trainer:
         self.freeze_encoder_bn = bool(tr.get("freeze_encoder_bn", False))
         self.freeze_all_bn = int(tr.get("freeze_all_bn", -1))
         self.epoch = 0
-        if precision not in ("fp32", "bf16"):
-            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        from .. import functional as mf
+        if precision not in mf.PRECISIONS:
+            raise ValueError(f"precision must be one of {mf.PRECISIONS}, got {precision!r}")
         self.precision = precision
         self.graph = bool(graph)
         if self.graph:

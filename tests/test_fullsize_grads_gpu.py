@@ -1,0 +1,123 @@
+"""Gradient parity at the benchmark shapes.
+
+The module- and toy-size model tests (test_models_gpu.py) never reach the GEMM paths the
+benchmark steps take: deep split-K weight gradients over ~10^5-10^6 pixels, the per-shape
+autotuned pipelining variants at the Swin stage-3/4 and DecoderBN shapes, K = 2224 convs.
+Here one full train-step backward of each model family runs at its BASELINE resolution
+and every parameter gradient is held to the fp64 CPU oracle (oracle/, pinned to the
+reference by tests/golden/):
+
+    max|g_gpu - g_64| <= 20 x max|g_cpu32 - g_64| + 1e-3 x max|g_64|
+
+per parameter (the 1e-3 gradient basis of test_models_gpu.py; 20 x the fp32 CPU oracle's
+own error covers gradients that are pure rounding noise in exact arithmetic, e.g. biases
+feeding a BatchNorm).  Forward outputs: 1e-4 relative (north_star's depth bar), or 20 x
+the fp32 oracle's error for the restated EfficientNet-B5 models (ill-conditioned BatchNorm
+stacks, see test_models_gpu._check_fwd_conditioned).
+
+Each test runs under the default matmul precision of the process (MDEMI_MATMUL_PRECISION:
+"fp32" exact-product MFMA, or "fp32e" three-plane bf16 MFMA)."""
+import pytest
+import torch
+
+from test_models_gpu import DEV, _check_fwd_conditioned, _check_param_grads, _filled_state, _no_dropout
+
+pytestmark = pytest.mark.gpu
+
+
+def test_large07_kitti_train_step_gradients():
+    """NeW-CRFs Swin-L (large07) at KITTI 352x1216 (BASELINE configs[2]), batch 1:
+    depth within 1e-4 relative and every parameter gradient vs the fp64 oracle."""
+    from mdemi.model.NewCRFs import NewCRFDepth
+    from oracle import newcrfs as onc
+    from oracle.weights import rng_array
+
+    torch.set_num_threads(16)
+    H, W = 352, 1216
+    m = NewCRFDepth(version="large07", max_depth=80.0, drop_path_rate=0.0)
+    sd = _filled_state(m, 0.13, 0.02)
+    m = m.to(DEV).train()
+    img = torch.from_numpy(rng_array((1, 3, H, W), 33))
+    depth = m(img.float().to(DEV))
+    dy = torch.from_numpy(rng_array((1, 1, H, W), 34))
+    (depth * dy.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+
+    def loss_fn(P):
+        dt = next(v.dtype for v in P.values() if torch.is_floating_point(v))
+        d = onc.newcrf_depth(P, img.to(dt), "large07", max_depth=80.0)
+        (d * dy.to(dt)).sum().backward()
+
+    assert _check_param_grads(m, sd, loss_fn, rel=1e-3) == len(list(m.parameters()))
+    with torch.no_grad():
+        ref = onc.newcrf_depth({k: v.double() if torch.is_floating_point(v) else v for k, v in sd.items()},
+                               img.double(), "large07", max_depth=80.0)
+    err = (depth.detach().double().cpu() - ref).abs().max().item()
+    assert err <= 1e-4 * ref.abs().max().item(), err
+
+
+def test_adabins_nyu_480x640_train_step_gradients():
+    """AdaBins-B5 at NYU 480x640 (BASELINE configs[1] resolution), batch 2: prediction, bin
+    edges and every parameter gradient vs the oracle."""
+    from mdemi.model.Adabins import UnetAdaptiveBins
+    from oracle import adabins as oab
+    from oracle.weights import rng_array
+
+    torch.set_num_threads(16)
+    m = UnetAdaptiveBins.build(256, 1e-3, 10.0)
+    sd = _filled_state(m, 0.43, 0.03)
+    _no_dropout(m)
+    m = m.to(DEV).train()
+    img = torch.from_numpy(rng_array((2, 3, 480, 640), 82))
+    pred, edges = m(img.float().to(DEV))
+    (pr, er), (pr32, er32) = (
+        _fwd(sd, dt, lambda P, dt: oab.unet_adaptive_bins(P, img.to(dt), 1e-3, 10.0)) for dt in (torch.float64,
+                                                                                                 torch.float32))
+    _check_fwd_conditioned("pred", pred, pr, pr32)
+    _check_fwd_conditioned("bin_edges", edges, er, er32)
+    dy = torch.from_numpy(rng_array(tuple(pr.shape), 83))
+    (pred * dy.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+
+    def loss_fn(P):
+        p, _ = oab.unet_adaptive_bins(P, img.to(P["conv_out.0.weight"].dtype), 1e-3, 10.0)
+        (p * dy.to(p.dtype)).sum().backward()
+
+    assert _check_param_grads(m, sd, loss_fn, rel=1e-3) == len(list(m.parameters()))
+
+
+def test_depthformer_v8_nyu_480x640_train_step_gradients():
+    """Depthformer v8 at NYU 480x640 with the benchmark's decoder width (hidden 256, 4 heads,
+    256 bins, 256 aux tokens), batch 2: depth, centres, the 8 attention maps and every
+    parameter gradient vs the oracle."""
+    from mdemi.model.Depthformer import DepthformerV8
+    from oracle import depthformer as odf
+    from oracle.weights import rng_array
+
+    torch.set_num_threads(16)
+    opt = {"hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256, "img_size": [480, 640],
+           "attn_drop_prob": 0.0, "drop_prob": 0.0}
+    m = DepthformerV8.build(opt, 1e-3, 10.0)
+    sd = _filled_state(m, 0.53, 0.03)
+    m = m.to(DEV).train()
+    img = torch.from_numpy(rng_array((2, 3, 480, 640), 84))
+    depth, centers, attn = m(img.float().to(DEV))
+    (dr, cr, ar), (dr32, cr32, ar32) = (
+        _fwd(sd, dt, lambda P, dt: odf.depthformer_v8_full(P, img.to(dt), opt, 1e-3, 10.0))
+        for dt in (torch.float64, torch.float32))
+    for i, (a, r, r32) in enumerate([(depth, dr, dr32), (centers, cr, cr32)] + list(zip(attn, ar, ar32))):
+        _check_fwd_conditioned(f"output {i}", a, r, r32)
+    dy = torch.from_numpy(rng_array(tuple(dr.shape), 85))
+    (depth * dy.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+
+    def loss_fn(P):
+        d, _, _ = odf.depthformer_v8_full(P, img.to(P["decoder.aux_embedding"].dtype), opt, 1e-3, 10.0)
+        (d * dy.to(d.dtype)).sum().backward()
+
+    assert _check_param_grads(m, sd, loss_fn, rel=1e-3) > 0
+
+
+def _fwd(sd, dtype, fn):
+    with torch.no_grad():
+        return fn({k: v.to(dtype) if torch.is_floating_point(v) else v for k, v in sd.items()}, dtype)
