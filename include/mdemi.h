@@ -136,8 +136,9 @@ int mdemi_gemm_f32e(const mdemi_gemm_desc* d, void* stream);
  * variants produce bit-identical results) and tile raster (group_m > 0:
  * XCD-aware grouped raster, 0: plain).  Process-global. */
 int mdemi_gemm_set_variant(int32_t variant, int32_t group_m);
-/* tuning hook of the 16-bit family (mdemi_gemm_bf16 / mdemi_gemm_f32e): 0 = two
- * LDS buffers, 1 = one, -1 = per-shape autotune (default; bit-identical). */
+/* tuning hook of the 16-bit family (mdemi_gemm_bf16 / mdemi_gemm_f32e): 0 = 128-row
+ * tile with two LDS buffers, 1 = one buffer, 2 = 256-row tile; -1 = per-shape
+ * autotune (default; all bit-identical). */
 int mdemi_gemm_set_variant_m16(int32_t variant);
 
 /* column / row sums (bias gradients: db[j] = sum_i dY[i][j])

@@ -343,7 +343,7 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
     p.fd_ow = make_fastdiv(g.ow); p.fd_oh = make_fastdiv(g.oh);
   }
   p.slab = nullptr;
-  p.tiles_m = (int)cdiv(d->M, GBM);
+  p.tiles_m = (int)cdiv(d->M, (mode != GEMM_F32 && variant == 2) ? 2 * GBM : GBM);  // 16-bit variant 2: 256 rows
   p.tiles_n = (int)cdiv(d->N, GBN);
   p.group_m = g_group_m;
 }
@@ -445,9 +445,9 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
   }
   if (!tunable(d, st)) return 0;
   static const int cands_f32[] = {0, 1, 3, 4, 5};
-  static const int cands_m16[] = {0, 1};
+  static const int cands_m16[] = {0, 1, 2};
   const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
-  const int ncand = mode != GEMM_F32 ? 2 : 5;
+  const int ncand = mode != GEMM_F32 ? 3 : 5;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 0;
   int best = 0;
@@ -489,7 +489,7 @@ extern "C" int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream) { return 
 extern "C" int mdemi_gemm_f32e(const mdemi_gemm_desc* d, void* stream) { return gemm_entry(d, stream, GEMM_F32E); }
 
 // Benchmark/tuning hook: force a pipelining variant of the fp32 family (see
-// pick_variant) and of the 16-bit family (0: two LDS buffers, 1: one; -1 =
+// pick_variant) and of the 16-bit family (gemm_mfma16.hip m16_variant; -1 =
 // per-shape autotune, the default) and the tile raster (group_m > 0: XCD-aware
 // grouped raster; 0: plain).
 extern "C" int mdemi_gemm_set_variant(int32_t variant, int32_t group_m) {
@@ -500,7 +500,7 @@ extern "C" int mdemi_gemm_set_variant(int32_t variant, int32_t group_m) {
 }
 
 extern "C" int mdemi_gemm_set_variant_m16(int32_t variant) {
-  MDEMI_REQUIRE(variant >= -1 && variant < 2, "gemm_set_variant_m16: bad variant");
+  MDEMI_REQUIRE(variant >= -1 && variant < 3, "gemm_set_variant_m16: bad variant");
   g_variant_m16 = variant;
   return MDEMI_OK;
 }

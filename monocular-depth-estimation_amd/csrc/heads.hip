@@ -255,14 +255,23 @@ __global__ __launch_bounds__(256) void binhead_nhwc_bwd_kernel(const float* __re
     part[((int64_t)b * nchunk + ch) * K + k] = (sred[k] + sred[K + k]) + (sred[2 * K + k] + sred[3 * K + k]);
 }
 
+// dcenters[b][k] = sum over chunks of part[b][chunk][k]: grid (ceil(K/64), B), lane = k,
+// wave w sums chunks w, w+4, ... (coalesced 256-B rows), then the 4 wave partials are
+// added in a fixed order through LDS (deterministic).
 __global__ __launch_bounds__(256) void binhead_nhwc_final(const float* __restrict__ part, float* __restrict__ dc,
                                                           int B, int K, int nchunk) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (int64_t)B * K) return;
-  const int b = (int)(e / K), k = (int)(e % K);
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int b = blockIdx.y, k = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int i = 0; i < nchunk; ++i) s += part[((int64_t)b * nchunk + i) * K + k];
-  dc[e] = s;
+  if (k < K) {
+    const float* pb = part + (int64_t)b * nchunk * K + k;
+#pragma unroll 4
+    for (int i = wid; i < nchunk; i += 4) s += pb[(int64_t)i * K];
+  }
+  red[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && k < K) dc[(int64_t)b * K + k] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 // ---------------------------------------------------------------------------
@@ -528,7 +537,7 @@ extern "C" int mdemi_binhead_nhwc_bwd(const float* logits, const float* centers,
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(binhead_nhwc_bwd_kernel, dim3(nchunk, B), dim3(256), 4 * K * sizeof(float), st, logits, centers,
                      pred, stats, dpred, dlogits, (float*)workspace, HW, K, nchunk);
-  hipLaunchKernelGGL(binhead_nhwc_final, dim3(grid_1d((int64_t)B * K)), dim3(256), 0, st, (const float*)workspace,
+  hipLaunchKernelGGL(binhead_nhwc_final, dim3((unsigned)cdiv(K, 64), B), dim3(256), 0, st, (const float*)workspace,
                      dcenters, B, K, nchunk);
   return check_launch("binhead_nhwc_bwd");
 }

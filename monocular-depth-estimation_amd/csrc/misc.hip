@@ -87,14 +87,29 @@ __global__ __launch_bounds__(OPT_THREADS) void sumsq_partial(const mdemi_tensor_
   const mdemi_tensor_ref t = tl[chunk_tensor[item]];
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
   const int64_t end = min(t.numel, beg + OPT_CHUNK);
-  float s = 0.f;
+  // four independent float4 streams per thread keep 4 loads in flight and 4 FMA chains
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
   const bool vec = ((uintptr_t)t.grad & 15) == 0;
   const int64_t vend = vec ? beg + ((end - beg) & ~(int64_t)3) : beg;
-  for (int64_t i = beg + 4 * threadIdx.x; i < vend; i += 4 * OPT_THREADS) {
-    const float4 g = *reinterpret_cast<const float4*>(t.grad + i);
-    s = fmaf(g.x, g.x, s); s = fmaf(g.y, g.y, s); s = fmaf(g.z, g.z, s); s = fmaf(g.w, g.w, s);
+  constexpr int64_t STEP = 4 * OPT_THREADS;
+  int64_t i = beg + 4 * threadIdx.x;
+  for (; i + 3 * STEP < vend; i += 4 * STEP) {
+    float4 g[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) g[u] = *reinterpret_cast<const float4*>(t.grad + i + u * STEP);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s4[u] = fmaf(g[u].x, g[u].x, s4[u]); s4[u] = fmaf(g[u].y, g[u].y, s4[u]);
+      s4[u] = fmaf(g[u].z, g[u].z, s4[u]); s4[u] = fmaf(g[u].w, g[u].w, s4[u]);
+    }
   }
-  for (int64_t i = vend + threadIdx.x; i < end; i += OPT_THREADS) s = fmaf(t.grad[i], t.grad[i], s);
+  for (; i < vend; i += STEP) {
+    const float4 g = *reinterpret_cast<const float4*>(t.grad + i);
+    s4[0] = fmaf(g.x, g.x, s4[0]); s4[0] = fmaf(g.y, g.y, s4[0]);
+    s4[0] = fmaf(g.z, g.z, s4[0]); s4[0] = fmaf(g.w, g.w, s4[0]);
+  }
+  for (int64_t j = vend + threadIdx.x; j < end; j += OPT_THREADS) s4[1] = fmaf(t.grad[j], t.grad[j], s4[1]);
+  float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   s = block_sum<OPT_THREADS>(s, red);
   if (threadIdx.x == 0) part[item] = s;
 }

@@ -38,34 +38,51 @@ __global__ __launch_bounds__(SL_THREADS) void silog_partial(const float* __restr
   }
 }
 
-// stats[g] = {n, mean, D, sqrt(D)}; loss = mean_g alpha*sqrt(D_g)
-__global__ void silog_finalize(const float* __restrict__ part, int nblk, int B, int per_image, int unbiased,
-                               float alpha, float beta, float* __restrict__ loss, float* __restrict__ stats) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// stats[g] = {n, mean, D, sqrt(D)}; loss = mean_g alpha*sqrt(D_g).  One block: the
+// partials of a group are summed by all threads in a fixed strided order, then a
+// fixed fp64 tree through LDS (deterministic, no serial pass over B x nblk partials).
+constexpr int SLF_THREADS = 256;
+__global__ __launch_bounds__(SLF_THREADS) void silog_finalize(const float* __restrict__ part, int nblk, int B,
+                                                              int per_image, int unbiased, float alpha, float beta,
+                                                              float* __restrict__ loss, float* __restrict__ stats) {
+  __shared__ double red[3][SLF_THREADS];
+  const int t = threadIdx.x;
   const int G = per_image ? B : 1;
   double total = 0.0;
   int used = 0;
   for (int g = 0; g < G; ++g) {
-    double n = 0, s1 = 0, s2 = 0;
     const int b0 = per_image ? g : 0, b1 = per_image ? g + 1 : B;
-    for (int b = b0; b < b1; ++b)
-      for (int i = 0; i < nblk; ++i) {
-        const float* o = part + ((int64_t)b * nblk + i) * 3;
-        n += o[0]; s1 += o[1]; s2 += o[2];
-      }
-    double mean = n > 0 ? s1 / n : 0.0, D = 0.0;
-    if (n > 0) {
-      const double var = unbiased ? (n > 1 ? (s2 - n * mean * mean) / (n - 1) : 0.0) : (s2 / n - mean * mean);
-      D = var + (double)beta * mean * mean;
-      total += (double)alpha * sqrt(D > 0 ? D : 0.0);
-      ++used;
+    const int64_t j0 = (int64_t)b0 * nblk, j1 = (int64_t)b1 * nblk;
+    double n = 0, s1 = 0, s2 = 0;
+    for (int64_t j = j0 + t; j < j1; j += SLF_THREADS) {
+      const float* o = part + j * 3;
+      n += o[0]; s1 += o[1]; s2 += o[2];
     }
-    stats[4 * g + 0] = (float)n;
-    stats[4 * g + 1] = (float)mean;
-    stats[4 * g + 2] = (float)D;
-    stats[4 * g + 3] = (float)sqrt(D > 0 ? D : 0.0);
+    red[0][t] = n; red[1][t] = s1; red[2][t] = s2;
+    __syncthreads();
+    for (int w = SLF_THREADS / 2; w > 0; w >>= 1) {
+      if (t < w) {
+        red[0][t] += red[0][t + w]; red[1][t] += red[1][t + w]; red[2][t] += red[2][t + w];
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      n = red[0][0]; s1 = red[1][0]; s2 = red[2][0];
+      double mean = n > 0 ? s1 / n : 0.0, D = 0.0;
+      if (n > 0) {
+        const double var = unbiased ? (n > 1 ? (s2 - n * mean * mean) / (n - 1) : 0.0) : (s2 / n - mean * mean);
+        D = var + (double)beta * mean * mean;
+        total += (double)alpha * sqrt(D > 0 ? D : 0.0);
+        ++used;
+      }
+      stats[4 * g + 0] = (float)n;
+      stats[4 * g + 1] = (float)mean;
+      stats[4 * g + 2] = (float)D;
+      stats[4 * g + 3] = (float)sqrt(D > 0 ? D : 0.0);
+    }
+    __syncthreads();
   }
-  loss[0] = used ? (float)(total / G) : 0.f;
+  if (t == 0) loss[0] = used ? (float)(total / G) : 0.f;
 }
 
 __global__ __launch_bounds__(SL_THREADS) void silog_bwd_kernel(const float* __restrict__ pred,
@@ -120,7 +137,7 @@ extern "C" int mdemi_silog_fwd(const float* pred, const float* gt, float* loss, 
   hipStream_t st = (hipStream_t)stream;
   const int nb = sl_blocks(HW);
   hipLaunchKernelGGL(silog_partial, dim3(nb, B), dim3(SL_THREADS), 0, st, pred, gt, (float*)workspace, HW, min_depth);
-  hipLaunchKernelGGL(silog_finalize, dim3(1), dim3(64), 0, st, (const float*)workspace, nb, B, per_image, unbiased,
+  hipLaunchKernelGGL(silog_finalize, dim3(1), dim3(SLF_THREADS), 0, st, (const float*)workspace, nb, B, per_image, unbiased,
                      alpha, beta, loss, stats);
   return check_launch("silog_fwd");
 }

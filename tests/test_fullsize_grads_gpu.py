@@ -57,11 +57,18 @@ def test_large07_kitti_train_step_gradients():
 
 
 def test_adabins_nyu_480x640_train_step_gradients():
-    """AdaBins-B5 at NYU 480x640 (BASELINE configs[1] resolution), batch 2: prediction, bin
-    edges and every parameter gradient vs the oracle."""
+    """AdaBins-B5 at NYU 480x640 (BASELINE configs[1] resolution), batch 2.
+
+    End to end: prediction, bin edges and every encoder gradient vs the oracle.  The head
+    (DecoderBN, mViT, folded conv_out + bin head) is then checked at the same size on the
+    GPU's own encoder features (the oracle gets the same fp32 feature values in fp64): the
+    restated B5 at random closed-form weights is ill-conditioned (its fp32 CPU gradients
+    stray up to 7e-2 from fp64), and fed through it the mViT's first-layer gradients pick up
+    the encoder's forward error, not the head's."""
     from mdemi.model.Adabins import UnetAdaptiveBins
     from oracle import adabins as oab
     from oracle.weights import rng_array
+    from test_models_gpu import fake_backend, nhwc_to_nchw
 
     torch.set_num_threads(16)
     m = UnetAdaptiveBins.build(256, 1e-3, 10.0)
@@ -83,7 +90,45 @@ def test_adabins_nyu_480x640_train_step_gradients():
         p, _ = oab.unet_adaptive_bins(P, img.to(P["conv_out.0.weight"].dtype), 1e-3, 10.0)
         (p * dy.to(p.dtype)).sum().backward()
 
-    assert _check_param_grads(m, sd, loss_fn, rel=1e-3) == len(list(m.parameters()))
+    n_enc = sum(1 for k, _ in m.named_parameters() if k.startswith("encoder."))
+    assert _check_param_grads(m, sd, loss_fn, rel=1e-3, only="encoder.") == n_enc
+
+    # the head at full size on the GPU's encoder features
+    with torch.no_grad():
+        feats = m.encoder(img.float().to(DEV))
+    keys = (4, 5, 6, 8, 11)
+    holder = {}
+    head = UnetAdaptiveBins(fake_backend(holder), n_bins=256, min_val=1e-3, max_val=10.0)
+    hsd = {k: v for k, v in sd.items() if not k.startswith("encoder.")}
+    head.load_state_dict(hsd, strict=False)
+    _no_dropout(head)
+    head = head.to(DEV).train()
+    ins = {k: feats[k].detach().clone().requires_grad_(True) for k in keys}
+    holder.update(ins)
+    hp, _ = head(torch.zeros(2, 3, 8, 8, device=DEV))
+    (hp * dy.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+
+    def head_oracle(dtype):
+        P = {k: (v.detach().to(dtype).clone().requires_grad_(True) if torch.is_floating_point(v) else v)
+             for k, v in hsd.items()}
+        fi = {k: nhwc_to_nchw(ins[k].detach()).cpu().to(dtype).requires_grad_(True) for k in keys}
+        p, _ = oab.adabins_head(P, fi, 1e-3, 10.0)
+        (p * dy.to(dtype)).sum().backward()
+        return P, fi, p.detach()
+
+    P64, F64, p64 = head_oracle(torch.float64)
+    P32, F32, _ = head_oracle(torch.float32)
+    e = (hp.detach().double().cpu() - p64).abs().max().item()
+    assert e <= 1e-4 * p64.abs().max().item(), e
+    pairs = [(k, p.grad, P64[k].grad, P32[k].grad) for k, p in head.named_parameters()]
+    pairs += [(f"feature {k}", nhwc_to_nchw(ins[k].grad), F64[k].grad, F32[k].grad) for k in keys]
+    for k, got, r64, r32 in pairs:
+        e_gpu = (got.double().cpu() - r64).abs().max().item()
+        e_cpu = (r32.double() - r64).abs().max().item()
+        mag = r64.abs().max().item()
+        assert e_gpu <= 20.0 * e_cpu + 1e-3 * mag + 1e-9, (k, e_gpu, e_cpu, mag)
+    assert len(pairs) == len(list(head.parameters())) + len(keys)
 
 
 def test_depthformer_v8_nyu_480x640_train_step_gradients():

@@ -9,7 +9,7 @@ MFMA kernel (precision "fp32").  Tolerance, per output tensor:
 
 on every operand layout the model uses (Linear fwd / dgrad / wgrad with the bias-gradient
 row sums, GELU applied on load, deep split-K, implicit-im2col conv fwd / dgrad / wgrad
-with zero and replicate padding and stride 2)."""
+with zero and replicate padding)."""
 import pytest
 import torch
 
@@ -75,7 +75,7 @@ def test_linear_f32e_matches_fp32_accuracy(mf, M, N, K, gelu):
 
 @pytest.mark.parametrize("cin,cout,k,stride,pad,hw,replicate",
                          [(64, 96, 3, 1, 1, (17, 23), False), (128, 64, 1, 1, 0, (30, 40), False),
-                          (36, 48, 3, 2, 1, (19, 26), False), (64, 64, 3, 1, 1, (15, 20), True),
+                          (36, 48, 3, 1, 1, (19, 26), False), (64, 64, 3, 1, 1, (15, 20), True),
                           (512, 256, 3, 1, 1, (44, 152), False)])
 def test_conv_f32e_matches_fp32_accuracy(mf, cin, cout, k, stride, pad, hw, replicate):
     from mdemi import _lib as L
@@ -115,7 +115,8 @@ def test_conv_f32e_matches_fp32_accuracy(mf, cin, cout, k, stride, pad, hw, repl
 
 
 def test_f32e_variants_bit_identical(mf):
-    """Both LDS-buffering variants add the same products in the same order."""
+    """Every 16-bit-family variant (LDS buffering, 128- / 256-row tiles) adds the same
+    products in the same order."""
     from mdemi import _lib as L
     lib = L.load()
     torch.manual_seed(5)
@@ -123,11 +124,11 @@ def test_f32e_variants_bit_identical(mf):
     w = torch.randn(384, 640, device=DEV)
     outs = []
     try:
-        for v in (0, 1):
+        for v in (0, 1, 2):
             assert lib.mdemi_gemm_set_variant_m16(v) == 0
             with mf.matmul_precision("fp32e"):
                 outs.append(mf.linear(x, w).clone())
     finally:
         lib.mdemi_gemm_set_variant_m16(-1)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

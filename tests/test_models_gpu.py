@@ -262,14 +262,17 @@ def _oracle_run(sd, dtype, loss_fn):
     return P, outs
 
 
-def _check_param_grads(model, sd, loss_fn, slack=20.0, rel=1e-4):
+def _check_param_grads(model, sd, loss_fn, slack=20.0, rel=1e-4, only=None):
     """GPU parameter gradients vs the fp64 oracle, within `slack` x the fp32 oracle's own error
     (BatchNorm stacks make some gradients -- e.g. biases feeding a BN, exactly zero in exact
-    arithmetic -- pure rounding noise) plus `rel` x the gradient's largest magnitude."""
+    arithmetic -- pure rounding noise) plus `rel` x the gradient's largest magnitude.
+    only: check the parameters whose names start with this prefix."""
     P64, _ = _oracle_run(sd, torch.float64, loss_fn)
     P32, _ = _oracle_run(sd, torch.float32, loss_fn)
     n = 0
     for k, p in model.named_parameters():
+        if only is not None and not k.startswith(only):
+            continue
         r64, r32 = P64[k].grad, P32[k].grad
         if r64 is None:
             assert p.grad is None or p.grad.abs().max().item() == 0, k
