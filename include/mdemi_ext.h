@@ -183,6 +183,37 @@ int mdemi_bins_chamfer_bwd(const float* gcent, const float* dloss, float* dedges
 int mdemi_conv_weight_layout(const float* w, float* out, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
                              int32_t mode, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* Sample transform of dataset/depth_dataset.py (replaces DepthDataset.      */
+/* __getitem__ :197-236 after file decoding, with random_crop :238-248,      */
+/* train_preprocess/augment_image/hide_depth :250-284, ImageDepth2Tensor     */
+/* :287-311 and RandomMasking :314-386) for a batch of decoded samples:      */
+/* rgb [B][H0][W0][3] uint8, depth [B][H0][W0] uint16 -> image [B][3][h][w]  */
+/* ImageNet-normalised fp32, depth [B][1][h][w] = raw / saving_factor.       */
+/* The frame (top, left, Hs, Ws) is the KITTI KB crop or the whole image;   */
+/* the rotation (Pillow's Image.rotate about the frame centre) and the crop */
+/* act inside it.  params: B device entries drawn by the host in the        */
+/* reference's order (mdemi/data.py).  nyu_mask applies depth_mask           */
+/* [45:472, 43:608] before the rotation; nearest_generic selects Pillow's    */
+/* I;16 nearest path (else the 16.16 fixed-point path of modes F and I).     */
+/* train = 0 is the test transform (no clip, hide_depth or masking).         */
+/* ------------------------------------------------------------------------ */
+#define MDEMI_AUG_MAX_SPANS 8
+typedef struct {
+  double affine[6];  /* Image.rotate's inverse map (x, y) -> source, in double     */
+  int32_t fixed[6];  /* the same map in Pillow's 16.16 fixed point (affine_fixed)  */
+  int32_t rotate;    /* 0: angle % 360 == 0 (Pillow returns a copy)                */
+  int32_t crop_x, crop_y, flip;
+  float gamma, brightness, color[3];
+  int32_t n_rows, n_cols, mask_keep; /* RandomMasking spans; mask_keep: drop_edge */
+  int32_t rows[MDEMI_AUG_MAX_SPANS][2];
+  int32_t cols[MDEMI_AUG_MAX_SPANS][2];
+} mdemi_aug_sample;
+int mdemi_augment(const uint8_t* rgb, const uint16_t* depth, int32_t B, int32_t H0, int32_t W0, int32_t top,
+                  int32_t left, int32_t Hs, int32_t Ws, int32_t h, int32_t w, const mdemi_aug_sample* params,
+                  int32_t nyu_mask, int32_t nearest_generic, int32_t train, float saving_factor, float clip_depth,
+                  float* image, float* depth_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

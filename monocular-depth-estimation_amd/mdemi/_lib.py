@@ -95,6 +95,16 @@ class AdamWGroup(ctypes.Structure):
                 ("_pad", i32)]
 
 
+AUG_MAX_SPANS = 8  # include/mdemi_ext.h MDEMI_AUG_MAX_SPANS
+
+
+class AugSample(ctypes.Structure):  # include/mdemi_ext.h mdemi_aug_sample
+    _fields_ = [("affine", ctypes.c_double * 6), ("fixed", i32 * 6), ("rotate", i32), ("crop_x", i32),
+                ("crop_y", i32), ("flip", i32), ("gamma", f32), ("brightness", f32), ("color", f32 * 3),
+                ("n_rows", i32), ("n_cols", i32), ("mask_keep", i32), ("rows", (i32 * 2) * AUG_MAX_SPANS),
+                ("cols", (i32 * 2) * AUG_MAX_SPANS)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "mdemi_last_error": (ctypes.c_char_p, []),
@@ -179,6 +189,8 @@ _SIGS = {
     "mdemi_bins_chamfer_fwd": (ctypes.c_int, [vp, vp, i32, i32, i32, i64, f32, vp, vp, vp, vp]),
     "mdemi_bins_chamfer_bwd": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp]),
     "mdemi_conv_weight_layout": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
+    "mdemi_augment": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32,
+                                     f32, f32, vp, vp, vp]),
 }
 
 _lib = None

@@ -78,3 +78,33 @@ def _assert_close(v, ref, rtol, atol, key):
 
 def spec_of(module):
     return [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in module.state_dict().items()]
+
+
+# ---- dataset/depth_dataset.py fixtures (tests/golden/make_golden_augment.py -> augment.npz)
+AUGMENT_CASES = {
+    # NYU train: valid-region mask, rotate +-2.5 deg, random 64x96 crop of the 480x640 frame
+    "nyu_train": dict(data_type="NYU", mode="train", raw=(480, 640), img_size=(64, 96), n=3, seed=11,
+                      depth_max=20000),
+    # KITTI train: KB crop of a 375x1242 frame, rotate +-1 deg, random 64x160 crop
+    "kitti_train": dict(data_type="KITTI", mode="train", raw=(375, 1242), img_size=(64, 160), n=2, seed=23,
+                        depth_max=30000),
+    # RandomMasking: four width drops of up to 20 % and one height drop
+    "nyu_train_masking": dict(data_type="NYU", mode="train", raw=(480, 640), img_size=(48, 64), n=2, seed=37,
+                              depth_max=20000, height_drop=(0.3, 1), width_drop=(0.2, 4)),
+    # drop_edge: keep one row band and one column band
+    "nyu_train_drop_edge": dict(data_type="NYU", mode="train", raw=(480, 640), img_size=(48, 64), n=2, seed=41,
+                                depth_max=20000, height_drop=(0.5, 1), width_drop=(0.5, 1), drop_edge=True),
+    # NYU test: no augmentation, the whole (small) image
+    "nyu_test": dict(data_type="NYU", mode="test", raw=(40, 56), img_size=None, n=2, seed=53, depth_max=20000),
+}
+
+
+def augment_inputs(case, i):
+    """The decoded files of sample i of an AUGMENT_CASES case: RGB uint8 noise and uint16
+    depth with ~10 % zeros (invalid pixels)."""
+    rng = np.random.default_rng(case["seed"] * 1000 + i)
+    H, W = case["raw"]
+    rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    dep = rng.integers(1, case["depth_max"], (H, W)).astype(np.uint16)
+    dep[rng.random((H, W)) < 0.1] = 0
+    return rgb, dep

@@ -60,11 +60,14 @@ def test_adabins_nyu_480x640_train_step_gradients():
     """AdaBins-B5 at NYU 480x640 (BASELINE configs[1] resolution), batch 2.
 
     End to end: prediction, bin edges and every encoder gradient vs the oracle.  The head
-    (DecoderBN, mViT, folded conv_out + bin head) is then checked at the same size on the
-    GPU's own encoder features (the oracle gets the same fp32 feature values in fp64): the
-    restated B5 at random closed-form weights is ill-conditioned (its fp32 CPU gradients
-    stray up to 7e-2 from fp64), and fed through it the mViT's first-layer gradients pick up
-    the encoder's forward error, not the head's."""
+    (DecoderBN, mViT, folded conv_out + bin head) is then checked at the same size on
+    seeded NHWC features of the encoder's shapes (the oracle gets the same fp32 values in
+    fp64).  Not on the restated B5's own features: at closed-form random weights several
+    up1 BatchNorm channels sit at the LeakyReLU kink (near-constant channels, beta ~ 0), so
+    which pixels take slope 1 or 0.01 flips with any fp32 forward rounding and those
+    channels' bias gradients are discontinuous in the inputs (tools/diag_head.py ... enc:
+    one of 97 gradients, up1._net.4.bias, lands at 1.8x the bound in exact-fp32 mode and
+    inside it in fp32e mode; on seeded features every gradient is within 0.34x of it)."""
     from mdemi.model.Adabins import UnetAdaptiveBins
     from oracle import adabins as oab
     from oracle.weights import rng_array
@@ -93,10 +96,11 @@ def test_adabins_nyu_480x640_train_step_gradients():
     n_enc = sum(1 for k, _ in m.named_parameters() if k.startswith("encoder."))
     assert _check_param_grads(m, sd, loss_fn, rel=1e-3, only="encoder.") == n_enc
 
-    # the head at full size on the GPU's encoder features
-    with torch.no_grad():
-        feats = m.encoder(img.float().to(DEV))
-    keys = (4, 5, 6, 8, 11)
+    # the head at full size on seeded features of the encoder's shapes (channels, stride)
+    chans = {4: (24, 2), 5: (40, 4), 6: (64, 8), 8: (176, 16), 11: (2048, 32)}
+    feats = {k: torch.from_numpy(rng_array((2, 480 // st, 640 // st, c), 90 + k)).float().to(DEV)
+             for k, (c, st) in chans.items()}
+    keys = tuple(chans)
     holder = {}
     head = UnetAdaptiveBins(fake_backend(holder), n_bins=256, min_val=1e-3, max_val=10.0)
     hsd = {k: v for k, v in sd.items() if not k.startswith("encoder.")}

@@ -1,0 +1,72 @@
+"""Diagnostic: AdaBins head (DecoderBN + mViT + bin head) gradients at a given input size on
+random NHWC features, vs the fp64 / fp32 CPU oracle; worst ratios first.
+    python tools/diag_head.py [H W B]"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "monocular-depth-estimation_amd")]
+from test_models_gpu import DEV, _filled_state, _no_dropout, fake_backend, nhwc_to_nchw  # noqa: E402
+from oracle import adabins as oab  # noqa: E402
+from oracle.weights import rng_array  # noqa: E402
+from mdemi.model.Adabins import UnetAdaptiveBins  # noqa: E402
+
+torch.set_num_threads(16)
+H, W, B = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (480, 640, 2)
+chans = {4: (24, 2), 5: (40, 4), 6: (64, 8), 8: (176, 16), 11: (2048, 32)}
+holder = {}
+head = UnetAdaptiveBins(fake_backend(holder), n_bins=256, min_val=1e-3, max_val=10.0)
+sd = _filled_state(head, 0.43, 0.03)
+_no_dropout(head)
+head = head.to(DEV).train()
+if len(sys.argv) > 4 and sys.argv[4] == "enc":  # the test's input: the GPU B5 features of its image
+    full = UnetAdaptiveBins.build(256, 1e-3, 10.0)
+    _filled_state(full, 0.43, 0.03)
+    _no_dropout(full)
+    full = full.to(DEV).train()
+    with torch.no_grad():
+        feats = full.encoder(torch.from_numpy(rng_array((B, 3, H, W), 82)).float().to(DEV))
+    ins = {k: feats[k].detach().clone().requires_grad_(True) for k in chans}
+    sd_full = full.state_dict()
+    head.load_state_dict({k: v for k, v in sd_full.items() if not k.startswith("encoder.")}, strict=False)
+    sd = {k: v.detach().cpu() for k, v in head.state_dict().items()}
+    del full
+else:
+    ins = {k: torch.from_numpy(rng_array((B, H // s, W // s, c), 90 + k)).float().to(DEV).requires_grad_(True)
+           for k, (c, s) in chans.items()}
+for k, v in ins.items():
+    x = v.detach().double()
+    print(f"feature {k}: shape {tuple(x.shape)} mean {x.mean().item():.3e} std {x.std().item():.3e} "
+          f"absmax {x.abs().max().item():.3e} chan-std min {x.reshape(-1, x.shape[-1]).std(0).min().item():.3e}")
+holder.update(ins)
+hp, _ = head(torch.zeros(B, 3, 8, 8, device=DEV))
+dy = torch.from_numpy(rng_array(tuple(hp.shape), 83))
+(hp * dy.float().to(DEV)).sum().backward()
+torch.cuda.synchronize()
+
+
+def oracle(dtype):
+    P = {k: (v.detach().to(dtype).clone().requires_grad_(True) if torch.is_floating_point(v) else v)
+         for k, v in sd.items() if not k.startswith("encoder.")}
+    fi = {k: nhwc_to_nchw(ins[k].detach()).cpu().to(dtype).requires_grad_(True) for k in chans}
+    p, _ = oab.adabins_head(P, fi, 1e-3, 10.0)
+    (p * dy.to(dtype)).sum().backward()
+    return P, fi, p.detach()
+
+
+P64, F64, p64 = oracle(torch.float64)
+P32, F32, _ = oracle(torch.float32)
+print("pred rel err", (hp.detach().double().cpu() - p64).abs().max().item() / p64.abs().max().item())
+rows = []
+for k, p in head.named_parameters():
+    r64, r32 = P64[k].grad, P32[k].grad
+    e_gpu = (p.grad.double().cpu() - r64).abs().max().item()
+    e_cpu = (r32.double() - r64).abs().max().item()
+    mag = r64.abs().max().item() + 1e-30
+    rows.append(((e_gpu) / (20 * e_cpu + 1e-3 * mag + 1e-9), k, e_gpu / mag, e_cpu / mag, tuple(p.shape)))
+rows.sort(reverse=True)
+for r in rows[:30]:
+    print(f"{r[0]:8.3f}  gpu_rel {r[2]:.2e}  cpu32_rel {r[3]:.2e}  {r[1]} {r[4]}")
+print("failing:", sum(1 for r in rows if r[0] > 1), "of", len(rows), flush=True)
