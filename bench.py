@@ -187,6 +187,60 @@ def _gemm_alg_bytes(A, B, M, N, K, kw):
     return b
 
 
+class _HbmTimers:
+    """HIP events around the bin head's forward and backward sweeps (mdemi_binhead_nhwc_fwd /
+    _bwd, SURVEY §8d's HBM-bound row) during the instrumented step; achieved GB/s from their
+    algorithmic bytes: fwd reads the logits and writes pred + the (max, sum) row stats,
+    4*B*HW*(K+3) B; bwd reads logits, pred, stats and dpred and writes dlogits,
+    4*B*HW*(2K+4) B."""
+
+    def __init__(self, mf):
+        self.cls = mf._BinHeadNHWCFn
+        self.orig = (self.cls.forward, self.cls.backward)
+        self.recs = {"binhead_nhwc_fwd": [], "binhead_nhwc_bwd": []}
+        f0, b0 = self.orig
+
+        def sizes(logits):
+            b, k = logits.shape[0], logits.shape[-1]
+            return b, logits[0].numel() // k, k
+
+        def fwd(ctx, logits, centers):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(torch.cuda.current_stream())
+            out = f0(ctx, logits, centers)
+            e.record(torch.cuda.current_stream())
+            b, hw, k = sizes(logits)
+            self.recs["binhead_nhwc_fwd"].append((4.0 * b * hw * (k + 3), s, e))
+            return out
+
+        def bwd(ctx, dpred):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(torch.cuda.current_stream())
+            out = b0(ctx, dpred)
+            e.record(torch.cuda.current_stream())
+            b, hw, k = sizes(ctx.saved_tensors[0])
+            self.recs["binhead_nhwc_bwd"].append((4.0 * b * hw * (2 * k + 4), s, e))
+            return out
+
+        self.cls.forward, self.cls.backward = staticmethod(fwd), staticmethod(bwd)
+
+    def restore(self):
+        self.cls.forward, self.cls.backward = staticmethod(self.orig[0]), staticmethod(self.orig[1])
+
+    def summary(self):
+        out = {}
+        for name, recs in self.recs.items():
+            if not recs:
+                continue
+            t = sum(s.elapsed_time(e) for _, s, e in recs) * 1e-3
+            by = sum(b for b, _, _ in recs)
+            out[name] = {"launches": len(recs), "avg_us": round(t / len(recs) * 1e6, 1),
+                         "algorithmic_bytes_per_launch": round(by / len(recs)),
+                         "achieved_GBps": round(by / t / 1e9, 1),
+                         "frac_of_hbm_peak": round(by / t / 1e9 / HBM_PEAK_GBS, 4)}
+        return out or None
+
+
 def gemm_roofline(trainer, batches):
     """One instrumented (eager, even for a captured trainer) step: HIP events around every
     libmdemi GEMM launch on its stream; algorithmic FLOPs (2*M*N*K per GEMM) and bytes /
@@ -205,12 +259,15 @@ def gemm_roofline(trainer, batches):
         return out
 
     mf.gemm = timed
+    hbm = _HbmTimers(mf)
     try:
         with mf.matmul_precision(trainer.precision):
             trainer._eager_step(batches)
         torch.cuda.synchronize()
     finally:
         mf.gemm = orig
+        hbm.restore()
+    trainer._hbm_kernels = hbm.summary()
     by = {}
     for key, fl, by_alg, s, e in recs:
         t = s.elapsed_time(e) * 1e-3
@@ -381,6 +438,8 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
                             "bus_GBps": round(2 * (world - 1) / world * sum(ddp.bucket_bytes) / (iso * 1e-3) / 1e9, 1)}
     if with_roofline:
         res["roofline"], res["extra"] = roofline_entry(trainer, batches, key, res["ms"])
+        if getattr(trainer, "_hbm_kernels", None):
+            res["extra"]["hbm_kernels"] = trainer._hbm_kernels
     return res
 
 

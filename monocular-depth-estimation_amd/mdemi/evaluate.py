@@ -95,16 +95,30 @@ class GraphedPredictor:
         return self.static_out.clone()
 
 
-def evaluate(model, batches, eval_opt, data_type):
+def evaluate(model, batches, eval_opt, data_type, weight_by_count=False):
     """Running mean of the metrics over (img, gt) batches on this rank, then the mean over ranks
-    (all_reduce_dict op="mean"; a pass-through without a process group)."""
+    (all_reduce_dict op="mean"; a pass-through without a process group).
+
+    The rank mean is unweighted, as all_reduce_dict(op="mean") makes it: exact when every
+    rank sees the same number of images (a padded DistributedSampler).  weight_by_count=True
+    instead reduces (sum, count) per metric and divides once -- the exact dataset mean when
+    ranks see different numbers of images (uneven last batch, no padding)."""
     was_training = model.training
     model.eval()
     avg = RunningAverageDict()
+    n = 0
     try:
         for img, gt in batches:
             for m in evaluate_batch(model, img, gt, eval_opt, data_type):
                 avg.update(m)
+                n += 1
     finally:
         model.train(was_training)
-    return all_reduce_dict(avg.get_value(), op="mean")
+    if not weight_by_count:
+        return all_reduce_dict(avg.get_value(), op="mean")
+    from .utils.depth_utils import METRICS
+    vals = avg.get_value() if n else {k: 0.0 for k in METRICS}  # every rank reduces the same keys
+    sums = {k: float(v) * n for k, v in vals.items()}
+    tot = all_reduce_dict({"__count": float(n), **sums}, op="sum")
+    count = tot.pop("__count")
+    return {k: v / count for k, v in tot.items()}

@@ -219,3 +219,29 @@ def test_grad_allreduce_launches_buckets_in_index_order():
         ar.finish()
     finally:
         dist.destroy_process_group()
+
+
+def _eval_weighting_worker(rank, world, init):
+    import torch.distributed as dist
+    from mdemi import evaluate as ev
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    try:
+        per_rank = [[1.0, 2.0, 3.0], [10.0]][rank]  # uneven: 3 images on rank 0, 1 on rank 1
+        ev_batch = ev.evaluate_batch
+        ev.evaluate_batch = lambda model, img, gt, opt, dt: [{"abs_rel": img}]
+        try:
+            class _M(torch.nn.Module):
+                pass
+            r_mean = ev.evaluate(_M(), [(v, None) for v in per_rank], {}, "NYU")
+            r_w = ev.evaluate(_M(), [(v, None) for v in per_rank], {}, "NYU", weight_by_count=True)
+        finally:
+            ev.evaluate_batch = ev_batch
+        assert abs(r_mean["abs_rel"] - (2.0 + 10.0) / 2) < 1e-9  # reference: mean of rank means
+        assert abs(r_w["abs_rel"] - 16.0 / 4) < 1e-9  # dataset mean
+    finally:
+        dist.destroy_process_group()
+
+
+def test_evaluate_rank_weighting(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_eval_weighting_worker, args=(2, f"file://{tmp_path}/rdzv"), nprocs=2, join=True)

@@ -16,7 +16,8 @@ import json
 import re
 import sys
 
-FAMILY = re.compile(r"gemm_f32_kernel<\d+, \d+, \d+, \d+,")
+FAMILY = re.compile(r"gemm_f32_kernel<\d+, \d+, \d+, \d+,|gemm_m16_kernel<\d+, \d+, \d+, \d+, \d+,|"
+                    r"winattn_\w+_kernel|binhead_nhwc_\w+")
 
 
 def per_family(path, counter, warmup):
@@ -49,7 +50,9 @@ def main():
         prof = json.load(open(out))
     except (OSError, ValueError):
         prof = {}
-    prof[workload] = {"families": fams,
+    old = prof.get(workload, {}).get("families", {})
+    old.update(fams)
+    prof[workload] = {"families": old,
                       "correction": "FETCH_SIZE x2 (gfx950 half-count of 16-B coalesced reads); KB->bytes x1024",
                       "source": note}
     json.dump(prof, open(out, "w"), indent=1)
