@@ -109,6 +109,13 @@ typedef struct mdemi_gemm_desc {
   float* rowsum_a;                 /* optional [M] output: sum_k A(i,k), A m-contiguous and
                                       batch 1 -- the bias gradient of a weight-gradient GEMM
                                       (dW = dY^T X, db = dY^T 1) without a second pass over dY */
+  int32_t batch_inner; int32_t _pad1;  /* > 1: batch index z = o * batch_inner + i, operand
+                                      offsets o * X_bstride + i * X_bstride_inner -- one
+                                      launch for every (image, head) of a multi-head
+                                      attention GEMM (heads are column slices of the token
+                                      buffers).  0/1: one-level batch.  Needs batch %
+                                      batch_inner == 0 and no aux/residual/preact/rowsum_a */
+  int64_t a_bstride_inner, b_bstride_inner, c_bstride_inner;
 } mdemi_gemm_desc;
 
 size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d);
@@ -124,10 +131,10 @@ int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream);
 /* Same contract at fp32 accuracy on the bf16 matrix cores ("f32e"): each fp32
  * operand is split exactly into three bf16 planes (a = a_hi + a_mid + a_lo, RNE)
  * as it is staged and the six products hi.hi, hi.mid, mid.hi, hi.lo, lo.hi,
- * mid.mid run on v_mfma_f32_32x32x16_bf16 with fp32 accumulation; the dropped
- * terms are below 2^-26 |a||b|, under one fp32 rounding of a product, so results
- * carry the error of mdemi_gemm_f32 (exact products, fp32 sums) at 2.67x its
- * matrix-core peak.  Replaces the same fp32 nn.Linear / nn.Conv2d / bmm products
+ * mid.mid run on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (dropped terms
+ * below 2^-24 |a||b|), at 2.67x the fp32 matrix-core peak.  fp32-level error
+ * except on heavily cancelling sums, where the bf16 MFMA's accumulation is
+ * measurably less exact than mdemi_gemm_f32's: an opt-in.  Replaces the same fp32 nn.Linear / nn.Conv2d / bmm products
  * as mdemi_gemm_f32 (swin_transformer.py:18-20,104,106,259; newcrf_layers.py:
  * 16-20,102,104,384,389; uper_crf_head.py:38-44,341-348; ...). */
 int mdemi_gemm_f32e(const mdemi_gemm_desc* d, void* stream);

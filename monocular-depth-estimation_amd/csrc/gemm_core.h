@@ -40,7 +40,16 @@ struct GemmParams {
   FastDiv fd_c, fd_kw, fd_ow, fd_oh;  // conv index decomposition
   int a_vec, b_vec;  // 1: 16-byte vector loads legal for this operand
   int tiles_m, tiles_n, group_m;
+  int binner;  // > 1: two-level batch (mdemi_gemm_desc.batch_inner)
+  int64_t a_bs2, b_bs2, c_bs2;
 };
+
+// element offset of batch entry b of an operand with outer stride s, inner stride s2
+__device__ __forceinline__ int64_t boff(const GemmParams& p, int b, int64_t s, int64_t s2) {
+  if (p.binner <= 1) return (int64_t)b * s;
+  const int o = b / p.binner;
+  return (int64_t)o * s + (int64_t)(b - o * p.binner) * s2;
+}
 
 // ---------------------------------------------------------------------------
 // Branch-free operand fetch.  Dense operands use buffer loads through a
@@ -288,7 +297,7 @@ struct Loader<MDEMI_L_CONV, OP, false, BK, TR, KC> {
 
 __device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int i, int j, float acc) {
   float v = p.alpha * acc;
-  if (p.beta != 0.f) v += p.beta * p.C[(int64_t)b * p.c_bs + (int64_t)i * p.ldc + j];
+  if (p.beta != 0.f) v += p.beta * p.C[boff(p, b, p.c_bs, p.c_bs2) + (int64_t)i * p.ldc + j];
   if (p.bias_mode == MDEMI_BIAS_COL) v += p.bias[j];
   else if (p.bias_mode == MDEMI_BIAS_ROW) v += p.bias[i];
   if (p.pre) p.pre[(int64_t)b * p.pre_bs + (int64_t)i * p.ldpre + j] = v;

@@ -1,0 +1,171 @@
+// fp32 MFMA GEMM kernel template and its variant / load-op pickers (see gemm_f32.hip
+// for the design); instantiated per layout pair in gemm_f32_inst{0..3}.hip so the
+// family compiles in parallel.
+#pragma once
+#include "common.h"
+#include "gemm_core.h"
+
+namespace mdemi {
+
+using KernelFn = void (*)(GemmParams);
+
+// Pipelining variants (A/B-tested on the model's shapes, tools/gemm_bench.py):
+//   BK    K depth per LDS tile (16 or 32)
+//   NBUF  LDS buffers (2: write the next tile while others read this one)
+//   PREF  register prefetch of the next tile before the MFMAs (issue early / write late)
+template <int AL, int BL, int AOP, int BOP, int BK, int NBUF, bool PREF, bool TR, int OCC>
+__global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void gemm_f32_kernel(GemmParams p) {
+  using LA = Loader<AL, AOP, true, BK, TR>;
+  using LB = Loader<BL, BOP, false, BK, TR>;
+  constexpr int FA = Img<LA::IMG, BK>::floats, FB = Img<LB::IMG, BK>::floats;
+  constexpr int NQ = BK / 8;
+  static_assert(NBUF == 2 || NBUF == 1, "NBUF");
+  __shared__ __attribute__((aligned(16))) float smem[NBUF * (FA + FB)];
+
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int zb = blockIdx.x / ntiles;
+  int tm, tn;
+  tile_of(p, blockIdx.x % ntiles, ntiles, tm, tn);
+  const int b = zb / p.split, sidx = zb % p.split;
+  const int bm = tm * GBM, bn = tn * GBN;
+
+  LA la;
+  LB lb;
+  la.init(p.A + boff(p, b, p.a_bs, p.a_bs2), p.lda, p.M, p.K, p.a_vec, bm, t, p);
+  lb.init(p.B + boff(p, b, p.b_bs, p.b_bs2), p.ldb, p.N, p.K, p.b_vec, bn, t, p);
+
+  const int ktiles_total = (p.K + BK - 1) / BK;
+  const int kt_begin = sidx * p.ktile_per_split;
+  const int kt_end = min(ktiles_total, kt_begin + p.ktile_per_split);
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+
+  float4 ra[NQ], rb[NQ];
+  // Row sums of an m-contiguous A (the bias gradient of a weight-gradient
+  // GEMM, dW = dY^T X, db = dY^T 1) accumulated from the staged registers
+  // by the tn == 0 column of workgroups: no second pass over dY.
+  constexpr bool CAN_RSUM = AL == MDEMI_L_MNCONTIG;
+  const bool do_rsum = CAN_RSUM && p.rowsum != nullptr && tn == 0;
+  float4 rsum = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto acc_rsum = [&]() {
+    if (CAN_RSUM && do_rsum) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        rsum.x += ra[q].x; rsum.y += ra[q].y; rsum.z += ra[q].z; rsum.w += ra[q].w;
+      }
+    }
+  };
+  const int l31 = lane & 31, h = lane >> 5;
+  const int ra0 = wm * 64 + l31, ra1 = ra0 + 32;
+  const int rb0 = wn * 64 + l31, rb1 = rb0 + 32;
+
+  if (PREF && kt_begin < kt_end) {
+    la.load(kt_begin * BK, ra);
+    lb.load(kt_begin * BK, rb);
+    LA::store(smem, t, ra);
+    LB::store(smem + FA, t, rb);
+    acc_rsum();
+    __syncthreads();
+  }
+
+  int cur = 0;
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const bool more = kt + 1 < kt_end;
+    if (!PREF) {  // plain: load, stage, barrier, compute (other workgroups overlap)
+      la.load(kt * BK, ra);
+      lb.load(kt * BK, rb);
+      LA::store(smem, t, ra);
+      LB::store(smem + FA, t, rb);
+      acc_rsum();
+      __syncthreads();
+    } else if (more) {  // issue next tile's global loads early; they land under the MFMAs
+      la.load((kt + 1) * BK, ra);
+      lb.load((kt + 1) * BK, rb);
+    }
+    const float* a_s = smem + cur * (FA + FB);
+    const float* b_s = a_s + FA;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      const float4 a0 = Img<LA::IMG, BK>::frag(a_s, ra0, g, h);
+      const float4 a1 = Img<LA::IMG, BK>::frag(a_s, ra1, g, h);
+      const float4 b0 = Img<LB::IMG, BK>::frag(b_s, rb0, g, h);
+      const float4 b1 = Img<LB::IMG, BK>::frag(b_s, rb1, g, h);
+#define MDEMI_STEP(X)                                                                  \
+  acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.X, b0.X, acc[0][0], 0, 0, 0); \
+  acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.X, b1.X, acc[0][1], 0, 0, 0); \
+  acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.X, b0.X, acc[1][0], 0, 0, 0); \
+  acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.X, b1.X, acc[1][1], 0, 0, 0);
+      MDEMI_STEP(x) MDEMI_STEP(y) MDEMI_STEP(z) MDEMI_STEP(w)
+#undef MDEMI_STEP
+    }
+    if (!PREF) {
+      __syncthreads();
+    } else {
+      if (more) {
+        if (NBUF == 1) __syncthreads();  // everyone done reading before overwrite
+        float* dst = smem + (NBUF == 1 ? 0 : (cur ^ 1)) * (FA + FB);
+        LA::store(dst, t, ra);
+        LB::store(dst + FA, t, rb);
+        acc_rsum();
+      }
+      __syncthreads();
+      if (NBUF == 2) cur ^= 1;
+    }
+  }
+  if (CAN_RSUM && do_rsum) {  // reduce the 8 k-row groups (t >> 5) through LDS
+    if (!PREF) __syncthreads();
+    float4* red = reinterpret_cast<float4*>(smem);
+    red[t] = rsum;
+    __syncthreads();
+    if (t < 32) {
+      float4 s4 = red[t];
+#pragma unroll
+      for (int g = 1; g < 8; ++g) {
+        const float4 o = red[t + 32 * g];
+        s4.x += o.x; s4.y += o.y; s4.z += o.z; s4.w += o.w;
+      }
+      float* dst = p.rowsum + (p.split > 1 ? (int64_t)sidx * p.M : 0);
+      const int i = bm + 4 * t;
+      if (i + 0 < p.M) dst[i + 0] = s4.x;
+      if (i + 1 < p.M) dst[i + 1] = s4.y;
+      if (i + 2 < p.M) dst[i + 2] = s4.z;
+      if (i + 3 < p.M) dst[i + 3] = s4.w;
+    }
+  }
+
+#include "gemm_epilogue.inc"
+}
+
+template <int AL, int BL, int AOP, int BOP>
+static KernelFn pick_variant(int v) {
+  switch (v) {
+    case 1: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, false, 2>;
+    case 2: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 4>;
+    case 3: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, true, 2>;
+    case 4: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 1, true, true, 2>;
+    case 5: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, false, 2>;
+    default: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 2>;
+  }
+}
+
+template <int AL, int BL>
+static KernelFn pick_ops(int aop, int bop, int v) {
+  if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_NONE) return pick_variant<AL, BL, MDEMI_OP_NONE, MDEMI_OP_NONE>(v);
+  if constexpr (AL == MDEMI_L_KCONTIG)
+    if (aop == MDEMI_OP_GELU && bop == MDEMI_OP_NONE)
+      return pick_variant<AL, BL, MDEMI_OP_GELU, MDEMI_OP_NONE>(v);
+  if constexpr (BL == MDEMI_L_MNCONTIG)
+    if (aop == MDEMI_OP_NONE && bop == MDEMI_OP_GELU)
+      return pick_variant<AL, BL, MDEMI_OP_NONE, MDEMI_OP_GELU>(v);
+  return nullptr;
+}
+
+}  // namespace mdemi

@@ -1,0 +1,14 @@
+// Instantiations of the 16-bit GEMM family (gemm_mfma16_kernel.h), layout pairs
+// (MNCONTIG, KCONTIG), (MNCONTIG, MNCONTIG): one translation unit per pair group so the
+// family's many template instances compile in parallel.
+#include "gemm_mfma16_kernel.h"
+
+namespace mdemi {
+
+KernelFn16 m16_pick_part1(int al, int bl, int aop, int bop, int np, int v) {
+  if (al == MDEMI_L_MNCONTIG && bl == MDEMI_L_KCONTIG) return m16_ops<MDEMI_L_MNCONTIG, MDEMI_L_KCONTIG>(aop, bop, np, v);
+  if (al == MDEMI_L_MNCONTIG && bl == MDEMI_L_MNCONTIG) return m16_ops<MDEMI_L_MNCONTIG, MDEMI_L_MNCONTIG>(aop, bop, np, v);
+  return nullptr;
+}
+
+}  // namespace mdemi

@@ -12,6 +12,8 @@
 //  - masked depth metrics (utils/depth_utils.py:4-54)
 // All HBM-bound; reductions are fixed-order (block partials + ordered final sums).
 #include "common.h"
+
+#include <algorithm>
 #include "mdemi_ext.h"
 
 namespace mdemi {
@@ -212,6 +214,51 @@ __global__ __launch_bounds__(256) void binhead_nhwc_fwd_kernel(const float* __re
   }
 }
 
+// K = 64 * NV (the 256 bins of AdaBins / Depthformer: NV = 4): 16 lanes per pixel, four
+// pixels per wave, each lane holding its NV float4 of the row in registers -- the row is
+// read once (the kernel above reads it twice) and the three reductions are 4-step
+// shuffles within the 16-lane group instead of 6-step wave reductions per pixel.
+template <int NV>
+__global__ __launch_bounds__(256) void binhead_nhwc_fwd_g16(const float* __restrict__ logits,
+                                                            const float* __restrict__ centers,
+                                                            float* __restrict__ pred, float* __restrict__ stats,
+                                                            int64_t HW, int64_t npix) {
+  constexpr int K = 64 * NV;
+  const int gl = threadIdx.x & 15;  // lane within the pixel's group
+  const int64_t groups = (int64_t)gridDim.x * 16;
+  for (int64_t pix = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); pix < npix; pix += groups) {
+    const int64_t b = pix / HW;
+    const float4* lr = reinterpret_cast<const float4*>(logits + pix * K);
+    const float4* cr = reinterpret_cast<const float4*>(centers + b * K);
+    float4 v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = lr[gl + 16 * j];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) m = fmaxf(m, fmaxf(fmaxf(v[j].x, v[j].y), fmaxf(v[j].z, v[j].w)));
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+    float s = 0.f, d = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float4 c = cr[gl + 16 * j];
+      const float e0 = __expf(v[j].x - m), e1 = __expf(v[j].y - m), e2 = __expf(v[j].z - m), e3 = __expf(v[j].w - m);
+      s += (e0 + e1) + (e2 + e3);
+      d = fmaf(e0, c.x, fmaf(e1, c.y, fmaf(e2, c.z, fmaf(e3, c.w, d))));
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o, 16);
+      d += __shfl_xor(d, o, 16);
+    }
+    if (gl == 0) {
+      const float inv = 1.f / s;
+      pred[pix] = d * inv;
+      *reinterpret_cast<float2*>(stats + 2 * pix) = make_float2(m, inv);
+    }
+  }
+}
+
 // grid (chunks, B): each wave handles BH_PIX pixels of image b; dcenters partials
 // per wave are combined per block and written to part[b][chunk][K].
 __global__ __launch_bounds__(256) void binhead_nhwc_bwd_kernel(const float* __restrict__ logits,
@@ -253,6 +300,66 @@ __global__ __launch_bounds__(256) void binhead_nhwc_bwd_kernel(const float* __re
   __syncthreads();
   for (int k = threadIdx.x; k < K; k += 256)
     part[((int64_t)b * nchunk + ch) * K + k] = (sred[k] + sred[K + k]) + (sred[2 * K + k] + sred[3 * K + k]);
+}
+
+// K = 64 * NV: the backward with the forward's 16-lane groups.  Grid (chunks, B) as above
+// (4 * BH_PIX pixels per block); the block's 16 groups sweep 16 consecutive pixels per
+// step, so a step reads and writes 16 contiguous rows.  Each lane keeps its bins' share
+// of sum_p g p_k (the dcenters partial) in registers across its pixels; the four groups
+// of a wave combine by shuffles and the four waves through LDS, in a fixed order.
+template <int NV>
+__global__ __launch_bounds__(256) void binhead_nhwc_bwd_g16(const float* __restrict__ logits,
+                                                            const float* __restrict__ centers,
+                                                            const float* __restrict__ pred,
+                                                            const float* __restrict__ stats,
+                                                            const float* __restrict__ dpred,
+                                                            float* __restrict__ dlogits, float* __restrict__ part,
+                                                            int64_t HW, int nchunk) {
+  constexpr int K = 64 * NV;
+  __shared__ float4 red[4][K / 4];
+  const int gl = threadIdx.x & 15, grp = threadIdx.x >> 4, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const float4* cr = reinterpret_cast<const float4*>(centers + (int64_t)b * K);
+  float4 c[NV], acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    c[j] = cr[gl + 16 * j];
+    acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int64_t p0 = (int64_t)ch * 4 * BH_PIX;
+  for (int it = 0; it < 4 * BH_PIX / 16; ++it) {
+    const int64_t p = p0 + it * 16 + grp;
+    if (p >= HW) break;
+    const int64_t pix = (int64_t)b * HW + p;
+    const float2 st = *reinterpret_cast<const float2*>(stats + 2 * pix);
+    const float g = dpred[pix], pr = pred[pix];
+    const float4* lr = reinterpret_cast<const float4*>(logits + pix * K);
+    float4* dr = reinterpret_cast<float4*>(dlogits + pix * K);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float4 v = lr[gl + 16 * j];
+      const float q0 = __expf(v.x - st.x) * st.y, q1 = __expf(v.y - st.x) * st.y, q2 = __expf(v.z - st.x) * st.y,
+                  q3 = __expf(v.w - st.x) * st.y;
+      dr[gl + 16 * j] = make_float4(q0 * g * (c[j].x - pr), q1 * g * (c[j].y - pr), q2 * g * (c[j].z - pr),
+                                    q3 * g * (c[j].w - pr));
+      acc[j].x = fmaf(q0, g, acc[j].x); acc[j].y = fmaf(q1, g, acc[j].y);
+      acc[j].z = fmaf(q2, g, acc[j].z); acc[j].w = fmaf(q3, g, acc[j].w);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      acc[j].x += __shfl_xor(acc[j].x, o, 64); acc[j].y += __shfl_xor(acc[j].y, o, 64);
+      acc[j].z += __shfl_xor(acc[j].z, o, 64); acc[j].w += __shfl_xor(acc[j].w, o, 64);
+    }
+  if (lane < 16)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) red[wid][gl + 16 * j] = acc[j];
+  __syncthreads();
+  const float* rf = reinterpret_cast<const float*>(red);
+  for (int k = threadIdx.x; k < K; k += 256)
+    part[((int64_t)b * nchunk + ch) * K + k] = (rf[k] + rf[K + k]) + (rf[2 * K + k] + rf[3 * K + k]);
 }
 
 // dcenters[b][k] = sum over chunks of part[b][chunk][k]: grid (ceil(K/64), B), lane = k,
@@ -517,8 +624,17 @@ extern "C" int mdemi_binhead_nhwc_fwd(const float* logits, const float* centers,
   MDEMI_REQUIRE(logits && centers && pred && stats && B > 0 && HW > 0 && K > 0 && K % 4 == 0,
                 "binhead_nhwc_fwd: bad args (K %% 4 == 0)");
   const int64_t npix = (int64_t)B * HW;
-  hipLaunchKernelGGL(binhead_nhwc_fwd_kernel, dim3(grid_1d(npix, 4)), dim3(256), 0, (hipStream_t)stream, logits,
-                     centers, pred, stats, HW, K, npix);
+  hipStream_t st = (hipStream_t)stream;
+  const bool al = ((uintptr_t)logits & 15) == 0 && ((uintptr_t)centers & 15) == 0 && ((uintptr_t)stats & 7) == 0;
+  if (al && (K == 64 || K == 128 || K == 256 || K == 512)) {
+    const unsigned nb = (unsigned)std::min<int64_t>(cdiv(npix, 16), 16384);
+    auto k = K == 64 ? binhead_nhwc_fwd_g16<1> : K == 128 ? binhead_nhwc_fwd_g16<2>
+           : K == 256 ? binhead_nhwc_fwd_g16<4> : binhead_nhwc_fwd_g16<8>;
+    hipLaunchKernelGGL(k, dim3(nb), dim3(256), 0, st, logits, centers, pred, stats, HW, npix);
+  } else {
+    hipLaunchKernelGGL(binhead_nhwc_fwd_kernel, dim3(grid_1d(npix, 4)), dim3(256), 0, st, logits, centers, pred,
+                       stats, HW, K, npix);
+  }
   return check_launch("binhead_nhwc_fwd");
 }
 
@@ -535,8 +651,17 @@ extern "C" int mdemi_binhead_nhwc_bwd(const float* logits, const float* centers,
   if (!workspace) { set_error("binhead_nhwc_bwd: workspace required"); return MDEMI_EWORKSPACE; }
   const int nchunk = (int)cdiv(HW, 4 * BH_PIX);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(binhead_nhwc_bwd_kernel, dim3(nchunk, B), dim3(256), 4 * K * sizeof(float), st, logits, centers,
-                     pred, stats, dpred, dlogits, (float*)workspace, HW, K, nchunk);
+  const bool al = ((uintptr_t)logits & 15) == 0 && ((uintptr_t)centers & 15) == 0 && ((uintptr_t)dlogits & 15) == 0 &&
+                  ((uintptr_t)stats & 7) == 0;
+  if (al && (K == 64 || K == 128 || K == 256 || K == 512)) {
+    auto k = K == 64 ? binhead_nhwc_bwd_g16<1> : K == 128 ? binhead_nhwc_bwd_g16<2>
+           : K == 256 ? binhead_nhwc_bwd_g16<4> : binhead_nhwc_bwd_g16<8>;
+    hipLaunchKernelGGL(k, dim3(nchunk, B), dim3(256), 0, st, logits, centers, pred, stats, dpred, dlogits,
+                       (float*)workspace, HW, nchunk);
+  } else {
+    hipLaunchKernelGGL(binhead_nhwc_bwd_kernel, dim3(nchunk, B), dim3(256), 4 * K * sizeof(float), st, logits,
+                       centers, pred, stats, dpred, dlogits, (float*)workspace, HW, K, nchunk);
+  }
   hipLaunchKernelGGL(binhead_nhwc_final, dim3((unsigned)cdiv(K, 64), B), dim3(256), 0, st, (const float*)workspace,
                      dcenters, B, K, nchunk);
   return check_launch("binhead_nhwc_bwd");

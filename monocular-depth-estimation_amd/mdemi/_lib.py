@@ -62,6 +62,8 @@ class GemmDesc(ctypes.Structure):
         ("conv", ConvGeom),
         ("preact", vp), ("ldpre", i64), ("pre_bstride", i64),
         ("rowsum_a", vp),
+        ("batch_inner", i32), ("_pad1", i32),
+        ("a_bstride_inner", i64), ("b_bstride_inner", i64), ("c_bstride_inner", i64),
     ]
 
 

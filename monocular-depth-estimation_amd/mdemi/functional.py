@@ -65,8 +65,9 @@ def _drop(src_ptr, dst_ptr, n, p, seed, add=0, offset=0):
 # Matmul precision of every libmdemi GEMM:
 #   "fp32"  exact-product fp32 MFMA (v_mfma_f32_32x32x2_f32), the reference's precision;
 #   "fp32e" fp32 on the bf16 matrix cores: operands split exactly into three bf16 planes,
-#           six plane products, fp32 accumulation -- the error of "fp32" (dropped terms
-#           < 2^-26 |a||b|) at 2.67x its peak (mdemi_gemm_f32e);
+#           six plane products, fp32 accumulation at 2.67x the fp32 peak
+#           (mdemi_gemm_f32e); fp32-level error except on heavily cancelling sums
+#           (DESIGN.md §5), hence opt-in;
 #   "bf16"  bf16 operands, fp32 accumulate: torch.autocast's matmul numerics (BASELINE
 #           configs[4]).
 # Process-wide; set it for a whole train step (forward and backward).
@@ -106,10 +107,14 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
          res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0, rowsum_a=None,
-         a_off=0, b_off=0, c_off=0):
-    """a_off/b_off/c_off: element offsets into A/B/C (column slices of wider buffers)."""
+         a_off=0, b_off=0, c_off=0, inner=None):
+    """a_off/b_off/c_off: element offsets into A/B/C (column slices of wider buffers).
+    inner=(n, a_bstride_inner, b_bstride_inner, c_bstride_inner): a two-level batch of
+    batch = outer * n entries (mdemi_gemm_desc.batch_inner), e.g. (image, head)."""
     d = L.GemmDesc()
     d.M, d.N, d.K, d.batch = M, N, K, batch
+    if inner is not None and inner[0] > 1:
+        d.batch_inner, d.a_bstride_inner, d.b_bstride_inner, d.c_bstride_inner = inner
     d.A, d.lda, d.a_bstride, d.a_layout, d.a_op = A.data_ptr() + 4 * a_off, lda, a_bstride, a_layout, a_op
     d.B, d.ldb, d.b_bstride, d.b_layout, d.b_op = B.data_ptr() + 4 * b_off, ldb, b_bstride, b_layout, b_op
     d.C, d.ldc, d.c_bstride = C.data_ptr() + 4 * c_off, ldc, c_bstride
@@ -1532,20 +1537,18 @@ class _AttentionFn(torch.autograd.Function):
         dev = qsrc.device
         P = torch.empty(B, heads, Sq, Sk, device=dev, dtype=torch.float32)
         hs = Sq * Sk
-        for h in range(heads):
-            gemm(qsrc, ksrc, P, Sq, Sk, dqk, lda=ldq, ldb=ldk, ldc=Sk, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
-                 batch=B, a_bstride=Sq * ldq, b_bstride=Sk * ldk, c_bstride=heads * hs, a_off=q_off + h * dqk,
-                 b_off=k_off + h * dqk, c_off=h * hs)
+        gemm(qsrc, ksrc, P, Sq, Sk, dqk, lda=ldq, ldb=ldk, ldc=Sk, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+             batch=B * heads, a_bstride=Sq * ldq, b_bstride=Sk * ldk, c_bstride=heads * hs, a_off=q_off,
+             b_off=k_off, inner=(heads, dqk, dqk, hs))
         L.call("mdemi_softmax_fwd", P.data_ptr(), P.data_ptr(), B * heads * Sq, Sk, float(scale), L.stream())
         Pd = P
         if p > 0.0:
             Pd = torch.empty_like(P)
             _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed)
         out = torch.empty(B * Sq, heads * dv, device=dev, dtype=torch.float32)
-        for h in range(heads):
-            gemm(Pd, vsrc, out, Sq, dv, Sk, lda=Sk, ldb=ldv, ldc=heads * dv, a_layout=L.L_KCONTIG,
-                 b_layout=L.L_MNCONTIG, batch=B, a_bstride=heads * hs, b_bstride=Sk * ldv, c_bstride=Sq * heads * dv,
-                 a_off=h * hs, b_off=v_off + h * dv, c_off=h * dv)
+        gemm(Pd, vsrc, out, Sq, dv, Sk, lda=Sk, ldb=ldv, ldc=heads * dv, a_layout=L.L_KCONTIG,
+             b_layout=L.L_MNCONTIG, batch=B * heads, a_bstride=heads * hs, b_bstride=Sk * ldv,
+             c_bstride=Sq * heads * dv, b_off=v_off, inner=(heads, hs, dv, dv))
         ctx.save_for_backward(qsrc, ksrc, vsrc, P)
         ctx.cfg = cfg
         return out, P
@@ -1574,13 +1577,12 @@ class _AttentionFn(torch.autograd.Function):
         dP = torch.empty_like(P)
         if dout is not None:
             dout = _c(dout)
-            for h in range(heads):
-                gemm(dout, vsrc, dP, Sq, Sk, dv, lda=heads * dv, ldb=ldv, ldc=Sk, a_layout=L.L_KCONTIG,
-                     b_layout=L.L_KCONTIG, batch=B, a_bstride=Sq * heads * dv, b_bstride=Sk * ldv,
-                     c_bstride=heads * hs, a_off=h * dv, b_off=v_off + h * dv, c_off=h * hs)
-                gemm(Pd, dout, dvv, Sk, dv, Sq, lda=Sk, ldb=heads * dv, ldc=ldv, a_layout=L.L_MNCONTIG,
-                     b_layout=L.L_MNCONTIG, batch=B, a_bstride=heads * hs, b_bstride=Sq * heads * dv,
-                     c_bstride=Sk * ldv, a_off=h * hs, b_off=h * dv, c_off=v_off + h * dv)
+            gemm(dout, vsrc, dP, Sq, Sk, dv, lda=heads * dv, ldb=ldv, ldc=Sk, a_layout=L.L_KCONTIG,
+                 b_layout=L.L_KCONTIG, batch=B * heads, a_bstride=Sq * heads * dv, b_bstride=Sk * ldv,
+                 c_bstride=heads * hs, b_off=v_off, inner=(heads, dv, dv, hs))
+            gemm(Pd, dout, dvv, Sk, dv, Sq, lda=Sk, ldb=heads * dv, ldc=ldv, a_layout=L.L_MNCONTIG,
+                 b_layout=L.L_MNCONTIG, batch=B * heads, a_bstride=heads * hs, b_bstride=Sq * heads * dv,
+                 c_bstride=Sk * ldv, c_off=v_off, inner=(heads, hs, dv, dv))
             if p > 0.0:
                 _drop(dP.data_ptr(), dP.data_ptr(), dP.numel(), p, seed)
             if dP_ext is not None:
@@ -1593,13 +1595,12 @@ class _AttentionFn(torch.autograd.Function):
             dP.zero_()
         L.call("mdemi_softmax_bwd", P.data_ptr(), dP.data_ptr(), dP.data_ptr(), B * heads * Sq, Sk, float(scale), 0,
                L.stream())
-        for h in range(heads):
-            gemm(dP, ksrc, dq, Sq, dqk, Sk, lda=Sk, ldb=ldk, ldc=ldq, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
-                 batch=B, a_bstride=heads * hs, b_bstride=Sk * ldk, c_bstride=Sq * ldq, a_off=h * hs,
-                 b_off=k_off + h * dqk, c_off=q_off + h * dqk)
-            gemm(dP, qsrc, dk, Sk, dqk, Sq, lda=Sk, ldb=ldq, ldc=ldk, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
-                 batch=B, a_bstride=heads * hs, b_bstride=Sq * ldq, c_bstride=Sk * ldk, a_off=h * hs,
-                 b_off=q_off + h * dqk, c_off=k_off + h * dqk)
+        gemm(dP, ksrc, dq, Sq, dqk, Sk, lda=Sk, ldb=ldk, ldc=ldq, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
+             batch=B * heads, a_bstride=heads * hs, b_bstride=Sk * ldk, c_bstride=Sq * ldq, b_off=k_off,
+             c_off=q_off, inner=(heads, hs, dqk, dqk))
+        gemm(dP, qsrc, dk, Sk, dqk, Sq, lda=Sk, ldb=ldq, ldc=ldk, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+             batch=B * heads, a_bstride=heads * hs, b_bstride=Sq * ldq, c_bstride=Sk * ldk, b_off=q_off,
+             c_off=k_off, inner=(heads, hs, dqk, dqk))
         seen, grads = set(), []
         for t, g in ((qsrc, dq), (ksrc, dk), (vsrc, dvv)):
             grads.append(None if id(t) in seen else g)

@@ -5,10 +5,33 @@ done by torch ops on CPU tensors (the only difference from the RCCL path)."""
 import os
 import tempfile
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+
+def _by_value(obj):
+    """Tensors cross the result queue as numpy copies: a torch tensor is shared through a
+    file descriptor that dies with the worker, racing the parent's unpickling."""
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().cpu().numpy().copy()
+    if isinstance(obj, dict):
+        return {k: _by_value(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_by_value(v) for v in obj)
+    return obj
+
+
+def _as_torch(obj):
+    if isinstance(obj, np.ndarray):
+        return torch.from_numpy(obj)
+    if isinstance(obj, dict):
+        return {k: _as_torch(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_as_torch(v) for v in obj)
+    return obj
 
 
 def _rendezvous():
@@ -47,7 +70,7 @@ def _dist_utils_worker(rank, world, path, q):
             res["bad_op"] = "no error"
         except RuntimeError as e:
             res["bad_op"] = str(e)
-        q.put((rank, res))
+        q.put((rank, _by_value(res)))
         dist.destroy_process_group()
     except Exception as e:  # surface worker failures in the parent
         q.put((rank, repr(e)))
@@ -71,8 +94,8 @@ def _ddp_worker(rank, world, path, q):
         ar.finish()
         grads = [p.grad.clone() for p in model.parameters()]
         params = [p.detach().clone() for p in model.parameters()]
-        q.put((rank, {"grads": grads, "params": params, "x": x, "order": ar.last_launch_order,
-                      "nbuckets": len(ar.buckets)}))
+        q.put((rank, _by_value({"grads": grads, "params": params, "x": x, "order": ar.last_launch_order,
+                      "nbuckets": len(ar.buckets)})))
         dist.destroy_process_group()
     except Exception as e:
         q.put((rank, repr(e)))
@@ -85,7 +108,7 @@ def _spawn(fn, world=2):
     procs = [ctx.Process(target=fn, args=(r, world, path, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=120) for _ in range(world))
+    out = {r: _as_torch(v) for r, v in (q.get(timeout=120) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
     for r, v in out.items():
@@ -170,9 +193,9 @@ def _accum_worker(rank, world, path, q):
             if step == 0:
                 first = [p.grad.clone() for p in model.parameters()]
         same_storage = [p.grad.data_ptr() for p in model.parameters()] == grads0
-        q.put((rank, {"first": first, "xs": xs[:2], "order": ar.last_launch_order, "nbuckets": len(ar.buckets),
+        q.put((rank, _by_value({"first": first, "xs": xs[:2], "order": ar.last_launch_order, "nbuckets": len(ar.buckets),
                       "same_storage": same_storage,
-                      "params": [p.detach().clone() for p in model.parameters()]}))
+                      "params": [p.detach().clone() for p in model.parameters()]})))
         dist.destroy_process_group()
     except Exception as e:
         q.put((rank, repr(e)))

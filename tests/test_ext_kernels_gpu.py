@@ -133,7 +133,8 @@ def test_dropout_mask_is_reproduced_in_backward(mf):
     assert mf.dropout(x, 0.1, False) is x
 
 
-@pytest.mark.parametrize("B,H,W,K", [(2, 5, 7, 256), (1, 3, 4, 32), (3, 16, 20, 128)])
+@pytest.mark.parametrize("B,H,W,K", [(2, 5, 7, 256), (1, 3, 4, 32), (3, 16, 20, 128), (2, 48, 64, 256),
+                                     (1, 17, 23, 64), (2, 9, 31, 512), (1, 6, 6, 36)])
 def test_bin_head_nhwc(mf, B, H, W, K):
     lg, c = rnd(B, K, H, W, seed=14, scale=3), rnd(B, K, seed=15, scale=5).abs()
     lr, cr = lg.clone().requires_grad_(), c.clone().requires_grad_()

@@ -15,8 +15,11 @@ feeding a BatchNorm).  Forward outputs: 1e-4 relative (north_star's depth bar), 
 the fp32 oracle's error for the restated EfficientNet-B5 models (ill-conditioned BatchNorm
 stacks, see test_models_gpu._check_fwd_conditioned).
 
-Each test runs under the default matmul precision of the process (MDEMI_MATMUL_PRECISION:
-"fp32" exact-product MFMA, or "fp32e" three-plane bf16 MFMA)."""
+The AdaBins and Depthformer tests run under the process's default matmul precision
+(MDEMI_MATMUL_PRECISION, "fp32" unless set); the KITTI test checks both fp32 modes.
+Under MDEMI_MATMUL_PRECISION=fp32e the Depthformer test misses the fp32 bar on one
+cancelling LayerNorm-bias gradient, as the KITTI test documents for large07
+(profiles/round2/fp32e8_suite.txt)."""
 import pytest
 import torch
 
@@ -26,11 +29,19 @@ pytestmark = pytest.mark.gpu
 
 
 def test_large07_kitti_train_step_gradients():
-    """NeW-CRFs Swin-L (large07) at KITTI 352x1216 (BASELINE configs[2]), batch 1:
-    depth within 1e-4 relative and every parameter gradient vs the fp64 oracle."""
+    """NeW-CRFs Swin-L (large07) at KITTI 352x1216 (BASELINE configs[2]), batch 1, vs the
+    fp64 oracle (computed once), in both fp32 matmul precisions:
+    * "fp32" (exact-product fp32 MFMA, the benchmark's): depth within 1e-4 relative and
+      every parameter gradient within 20x the fp32 CPU error + 1e-3 of its magnitude;
+    * "fp32e" (opt-in, three bf16 planes on the bf16 matrix cores): depth within 1e-4 and
+      every gradient within 1e-2 of its magnitude -- its cancelling LayerNorm-bias sums
+      miss the fp32 bar (4.5e-3 relative measured, profiles/round2/fp32e_parity_tests.txt),
+      so this bounds the opt-in mode's error profile rather than claiming fp32's."""
+    from mdemi import functional as mf
     from mdemi.model.NewCRFs import NewCRFDepth
     from oracle import newcrfs as onc
     from oracle.weights import rng_array
+    from test_models_gpu import _oracle_run
 
     torch.set_num_threads(16)
     H, W = 352, 1216
@@ -38,22 +49,34 @@ def test_large07_kitti_train_step_gradients():
     sd = _filled_state(m, 0.13, 0.02)
     m = m.to(DEV).train()
     img = torch.from_numpy(rng_array((1, 3, H, W), 33))
-    depth = m(img.float().to(DEV))
     dy = torch.from_numpy(rng_array((1, 1, H, W), 34))
-    (depth * dy.float().to(DEV)).sum().backward()
-    torch.cuda.synchronize()
 
     def loss_fn(P):
         dt = next(v.dtype for v in P.values() if torch.is_floating_point(v))
         d = onc.newcrf_depth(P, img.to(dt), "large07", max_depth=80.0)
         (d * dy.to(dt)).sum().backward()
+        return d.detach()
 
-    assert _check_param_grads(m, sd, loss_fn, rel=1e-3) == len(list(m.parameters()))
-    with torch.no_grad():
-        ref = onc.newcrf_depth({k: v.double() if torch.is_floating_point(v) else v for k, v in sd.items()},
-                               img.double(), "large07", max_depth=80.0)
-    err = (depth.detach().double().cpu() - ref).abs().max().item()
-    assert err <= 1e-4 * ref.abs().max().item(), err
+    P64, ref = _oracle_run(sd, torch.float64, loss_fn)
+    P32, _ = _oracle_run(sd, torch.float32, loss_fn)
+    for prec in ("fp32", "fp32e"):
+        m.zero_grad(set_to_none=True)
+        with mf.matmul_precision(prec):
+            depth = m(img.float().to(DEV))
+            (depth * dy.float().to(DEV)).sum().backward()
+        torch.cuda.synchronize()
+        err = (depth.detach().double().cpu() - ref).abs().max().item()
+        assert err <= 1e-4 * ref.abs().max().item(), (prec, err)
+        n = 0
+        for k, p in m.named_parameters():
+            r64, r32 = P64[k].grad, P32[k].grad
+            e_gpu = (p.grad.double().cpu() - r64).abs().max().item()
+            e_cpu = (r32.double() - r64).abs().max().item()
+            mag = r64.abs().max().item()
+            lim = 20.0 * e_cpu + 1e-3 * mag + 1e-9 if prec == "fp32" else 1e-2 * mag + 1e-9
+            assert e_gpu <= lim, (prec, k, e_gpu, e_cpu, mag)
+            n += 1
+        assert n == len(list(m.parameters()))
 
 
 def test_adabins_nyu_480x640_train_step_gradients():
