@@ -111,6 +111,15 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     """a_off/b_off/c_off: element offsets into A/B/C (column slices of wider buffers).
     inner=(n, a_bstride_inner, b_bstride_inner, c_bstride_inner): a two-level batch of
     batch = outer * n entries (mdemi_gemm_desc.batch_inner), e.g. (image, head)."""
+    if inner is not None and inner[0] > 1 and os.environ.get("MDEMI_GEMM_SPLIT_INNER") == "1":
+        # debug/A-B path: the same products as one launch per inner index
+        n, a2, b2, c2 = inner
+        for i in range(n):
+            gemm(A, B, C, M, N, K, lda=lda, ldb=ldb, ldc=ldc, a_layout=a_layout, b_layout=b_layout, a_op=a_op,
+                 b_op=b_op, alpha=alpha, beta=beta, bias=bias, bias_mode=bias_mode, act=act, batch=batch // n,
+                 a_bstride=a_bstride, b_bstride=b_bstride, c_bstride=c_bstride, split_k=split_k, conv=conv,
+                 a_off=a_off + i * a2, b_off=b_off + i * b2, c_off=c_off + i * c2)
+        return C
     d = L.GemmDesc()
     d.M, d.N, d.K, d.batch = M, N, K, batch
     if inner is not None and inner[0] > 1:

@@ -387,3 +387,25 @@ def test_bins_chamfer_loss_from_centres(mf):
     got.backward()
     close(got, d_ref.detach(), rtol=1e-5, atol=1e-7)
     close(cg.grad.view(B, P), cr.grad, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_gemm_two_level_batch(mf, prec):
+    """batch_inner: entry z = o * n + i reads A at o*sa + i*sa2, B at o*sb + i*sb2 and writes C at
+    o*sc + i*sc2 -- per-head column slices of token-major buffers, as the attention op uses."""
+    from mdemi import _lib as L
+    Bo, n, M, N, K = 3, 4, 37, 24, 20
+    A = rnd(Bo * M, n * K + 4, seed=60).float().to(DEV)        # [B*M, heads*K (+4 unused)]
+    Bm = rnd(Bo * N, n * K, seed=61).float().to(DEV)           # [B*N, heads*K]
+    C = torch.full((Bo, n, M, N), float("nan"), device=DEV)
+    with mf.matmul_precision(prec):
+        mf.gemm(A, Bm, C, M, N, K, lda=n * K + 4, ldb=n * K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+                batch=Bo * n, a_bstride=M * (n * K + 4), b_bstride=N * n * K, c_bstride=n * M * N, a_off=4,
+                inner=(n, K, K, M * N))
+    torch.cuda.synchronize()
+    Ar = A[:, 4:].double().cpu().view(Bo, M, n, K).transpose(1, 2)
+    Br = Bm.double().cpu().view(Bo, N, n, K).transpose(1, 2)
+    ref = Ar @ Br.transpose(-1, -2)
+    tol = 1e-5 if prec == "fp32" else 2e-2
+    assert torch.isfinite(C).all()
+    close(C, ref, rtol=tol)

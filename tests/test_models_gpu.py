@@ -530,3 +530,18 @@ def test_graphed_predictor_matches_eager():
         want = predict_depth(m, x, flip_eval=True)
         torch.cuda.synchronize()
         assert torch.equal(got, want)
+    # eager work at a larger shape after the capture grows the shared workspaces (split-K
+    # slabs, attention scratch): the graph must keep replaying into buffers that stay alive
+    big = torch.from_numpy(rng_array((4, 3, 128, 192), 5)).float().to(DEV)
+    m.train()
+    (m(big) * 1.0).sum().backward()
+    m.eval()
+    m.zero_grad(set_to_none=True)
+    want_big = predict_depth(m, big, flip_eval=True)
+    junk = [torch.full((1 << 20,), float("nan"), device=DEV) for _ in range(8)]  # reuse freed blocks
+    for x in (a, b):
+        got = gp(x)
+        want = predict_depth(m, x, flip_eval=True)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want)
+    assert torch.isfinite(want_big).all() and len(junk) == 8

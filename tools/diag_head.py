@@ -18,7 +18,14 @@ H, W, B = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (480, 640, 2
 chans = {4: (24, 2), 5: (40, 4), 6: (64, 8), 8: (176, 16), 11: (2048, 32)}
 holder = {}
 head = UnetAdaptiveBins(fake_backend(holder), n_bins=256, min_val=1e-3, max_val=10.0)
-sd = _filled_state(head, 0.43, 0.03)
+if len(sys.argv) > 4 and sys.argv[4] == "testfill":  # the weights of test_adabins_nyu_480x640_*: full-model fill
+    full = UnetAdaptiveBins.build(256, 1e-3, 10.0)
+    fsd = _filled_state(full, 0.43, 0.03)
+    head.load_state_dict({k: v for k, v in fsd.items() if not k.startswith("encoder.")}, strict=False)
+    del full
+    sd = {k: v.detach().cpu().clone() for k, v in head.state_dict().items()}
+else:
+    sd = _filled_state(head, 0.43, 0.03)
 _no_dropout(head)
 head = head.to(DEV).train()
 if len(sys.argv) > 4 and sys.argv[4] == "enc":  # the test's input: the GPU B5 features of its image

@@ -14,3 +14,6 @@ timeout -k 10 400 python -u bench.py --model depthformer --no-cpu-baseline > gpu
 grep '^{"metric' gpurun_out/bench_dfv8_g.log
 timeout -k 10 400 python -u bench.py --model depthformer_bf16 --no-cpu-baseline > gpurun_out/bench_dfv8bf16_g.log 2>&1 || { tail -20 gpurun_out/bench_dfv8bf16_g.log; exit 1; }
 grep '^{"metric' gpurun_out/bench_dfv8bf16_g.log
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --kernel-include-regex gemm_f32_kernel -d gpurun_out/f32_pmc1 -o run --output-format csv -- python3 tools/m16_bench.py 3 > gpurun_out/f32_pmc1.log 2>&1 || { tail -5 gpurun_out/f32_pmc1.log; exit 1; }
+echo pmc done
