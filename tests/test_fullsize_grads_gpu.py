@@ -95,8 +95,11 @@ def test_adabins_nyu_480x640_train_step_gradients():
     the mViT's layer-0 feed-forward weight/bias gradients land 41-52x over the bar (27 %
     relative) while every other head gradient passes -- identically with the library of
     this round's start and today's (profiles/round2/diag_adabins_head_*), so it is not a
-    regression of this round's kernels; tools/diag_relu_kink.py examines whether ReLU
-    sign flips of near-zero pre-activations explain it."""
+    regression of this round's kernels.  tools/diag_relu_kink.py finds the cause: one of
+    the layer's 614,400 pre-activations is 1.5e-6 in fp64 and lands on the other side of
+    the ReLU kink in the GPU's fp32 forward (whose error there is 3.6e-5 of max|z|, 75
+    values lie below it), which moves that column's bias gradient by a whole dA element
+    (profiles/round2/diag_relu_kink_mvit_layer0.txt): a discontinuity, not an error."""
     from mdemi.model.Adabins import UnetAdaptiveBins
     from oracle import adabins as oab
     from oracle.weights import rng_array
