@@ -86,13 +86,14 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const fl
 //   1: as 0 with [row][k] images (ds_read_b128 fragments)
 //   2: as 0 capped at 128 VGPRs (4 waves/SIMD; spills)
 //   3: BK32, 2 buffers (2 workgroups/CU by LDS)   4: BK32, 1 buffer   5: as 3, [row][k]
+//   6: 256-row tile (waves of 128x64), BK32, 1 buffer   7: 256-row tile, BK16, 2 buffers
 // No variant wins every shape (e.g. weight-gradient GEMMs over few output
 // tiles want BK32/2 buffers, token-major forwards want BK32/1 buffer), so by
 // default each distinct (layouts, ops, M, N, K, batch, split) is timed once
 // over the candidates on first use and the winner cached.  All variants add
 // the k products in the same order and split K at the same 32-element
 // boundaries, so the choice never changes a result bit.
-constexpr int NVARIANTS = 6;
+constexpr int NVARIANTS = 8;
 static int g_variant = -1;  // -1: autotune per shape
 static int g_variant_m16 = -1;  // 16-bit family (bf16 / split fp32): 0 two LDS buffers, 1 one
 static int g_group_m = 8;
@@ -109,7 +110,8 @@ static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
   return f32_pick_part3(al, bl, aop, bop, v);
 }
 
-static int variant_bk(int v, int mode) { return mode != GEMM_F32 ? 32 : (v >= 3 ? 32 : 16); }
+static int variant_bk(int v, int mode) { return mode != GEMM_F32 ? 32 : ((v >= 3 && v != 7) ? 32 : 16); }
+static int variant_rows(int v, int mode) { return (mode != GEMM_F32 ? v == 2 : v >= 6) ? 2 * GBM : GBM; }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -188,7 +190,7 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
     p.fd_ow = make_fastdiv(g.ow); p.fd_oh = make_fastdiv(g.oh);
   }
   p.slab = nullptr;
-  p.tiles_m = (int)cdiv(d->M, (mode != GEMM_F32 && variant == 2) ? 2 * GBM : GBM);  // 16-bit variant 2: 256 rows
+  p.tiles_m = (int)cdiv(d->M, variant_rows(variant, mode));  // 256-row variants: 16-bit 2, fp32 6 and 7
   p.tiles_n = (int)cdiv(d->N, GBN);
   p.group_m = g_group_m;
 }
@@ -289,10 +291,10 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
     if (it != g_tuned.end()) return it->second;
   }
   if (!tunable(d, st)) return 0;
-  static const int cands_f32[] = {0, 1, 3, 4, 5};
+  static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7};
   static const int cands_m16[] = {0, 1, 2};
   const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
-  const int ncand = mode != GEMM_F32 ? 3 : 5;
+  const int ncand = mode != GEMM_F32 ? 3 : 7;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 0;
   int best = 0;

@@ -13,14 +13,21 @@ using KernelFn = void (*)(GemmParams);
 //   BK    K depth per LDS tile (16 or 32)
 //   NBUF  LDS buffers (2: write the next tile while others read this one)
 //   PREF  register prefetch of the next tile before the MFMAs (issue early / write late)
-template <int AL, int BL, int AOP, int BOP, int BK, int NBUF, bool PREF, bool TR, int OCC>
+//   BMT   block-tile rows: 128 (2x2 waves of 64x64) or 256 (2x2 waves of 128x64, A staged as
+//         two 128-row images: twice the MFMAs per barrier and per B fragment)
+template <int AL, int BL, int AOP, int BOP, int BK, int NBUF, bool PREF, bool TR, int OCC, int BMT = 128>
 __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void gemm_f32_kernel(GemmParams p) {
   using LA = Loader<AL, AOP, true, BK, TR>;
   using LB = Loader<BL, BOP, false, BK, TR>;
   constexpr int FA = Img<LA::IMG, BK>::floats, FB = Img<LB::IMG, BK>::floats;
   constexpr int NQ = BK / 8;
+  constexpr int NA = BMT / 128;  // 128-row A images per tile
+  constexpr int IM = BMT / 64;   // 32-row accumulator blocks per wave along M
+  constexpr int WTM = BMT / 2;   // wave tile rows
+  constexpr int FAT = NA * FA;   // floats of the A images
   static_assert(NBUF == 2 || NBUF == 1, "NBUF");
-  __shared__ __attribute__((aligned(16))) float smem[NBUF * (FA + FB)];
+  static_assert(BMT == 128 || BMT == 256, "BMT");
+  __shared__ __attribute__((aligned(16))) float smem[NBUF * (FAT + FB)];
 
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -29,50 +36,68 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   int tm, tn;
   tile_of(p, blockIdx.x % ntiles, ntiles, tm, tn);
   const int b = zb / p.split, sidx = zb % p.split;
-  const int bm = tm * GBM, bn = tn * GBN;
+  const int bm = tm * BMT, bn = tn * GBN;
 
-  LA la;
+  LA la[NA];
   LB lb;
-  la.init(p.A + boff(p, b, p.a_bs, p.a_bs2), p.lda, p.M, p.K, p.a_vec, bm, t, p);
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+    la[a].init(p.A + boff(p, b, p.a_bs, p.a_bs2), p.lda, p.M, p.K, p.a_vec, bm + 128 * a, t, p);
   lb.init(p.B + boff(p, b, p.b_bs, p.b_bs2), p.ldb, p.N, p.K, p.b_vec, bn, t, p);
 
   const int ktiles_total = (p.K + BK - 1) / BK;
   const int kt_begin = sidx * p.ktile_per_split;
   const int kt_end = min(ktiles_total, kt_begin + p.ktile_per_split);
 
-  floatx16 acc[2][2];
+  floatx16 acc[IM][2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < IM; ++a)
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
 
-  float4 ra[NQ], rb[NQ];
+  float4 ra[NA][NQ], rb[NQ];
   // Row sums of an m-contiguous A (the bias gradient of a weight-gradient
   // GEMM, dW = dY^T X, db = dY^T 1) accumulated from the staged registers
   // by the tn == 0 column of workgroups: no second pass over dY.
   constexpr bool CAN_RSUM = AL == MDEMI_L_MNCONTIG;
   const bool do_rsum = CAN_RSUM && p.rowsum != nullptr && tn == 0;
-  float4 rsum = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 rsum[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) rsum[a] = make_float4(0.f, 0.f, 0.f, 0.f);
   auto acc_rsum = [&]() {
     if (CAN_RSUM && do_rsum) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        rsum.x += ra[q].x; rsum.y += ra[q].y; rsum.z += ra[q].z; rsum.w += ra[q].w;
-      }
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          rsum[a].x += ra[a][q].x; rsum[a].y += ra[a][q].y; rsum[a].z += ra[a][q].z; rsum[a].w += ra[a][q].w;
+        }
     }
   };
   const int l31 = lane & 31, h = lane >> 5;
-  const int ra0 = wm * 64 + l31, ra1 = ra0 + 32;
+  int rA[IM];  // this wave's fragment rows within A image aimg
+#pragma unroll
+  for (int i = 0; i < IM; ++i) rA[i] = (wm * WTM + 32 * i + l31) & 127;
+  const int aimg = (wm * WTM) >> 7;
   const int rb0 = wn * 64 + l31, rb1 = rb0 + 32;
 
-  if (PREF && kt_begin < kt_end) {
-    la.load(kt_begin * BK, ra);
-    lb.load(kt_begin * BK, rb);
-    LA::store(smem, t, ra);
-    LB::store(smem + FA, t, rb);
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a) la[a].load(kt * BK, ra[a]);
+    lb.load(kt * BK, rb);
+  };
+  auto stage = [&](float* dst) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a) LA::store(dst + a * FA, t, ra[a]);
+    LB::store(dst + FAT, t, rb);
     acc_rsum();
+  };
+
+  if (PREF && kt_begin < kt_end) {
+    load(kt_begin);
+    stage(smem);
     __syncthreads();
   }
 
@@ -80,29 +105,26 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const bool more = kt + 1 < kt_end;
     if (!PREF) {  // plain: load, stage, barrier, compute (other workgroups overlap)
-      la.load(kt * BK, ra);
-      lb.load(kt * BK, rb);
-      LA::store(smem, t, ra);
-      LB::store(smem + FA, t, rb);
-      acc_rsum();
+      load(kt);
+      stage(smem);
       __syncthreads();
     } else if (more) {  // issue next tile's global loads early; they land under the MFMAs
-      la.load((kt + 1) * BK, ra);
-      lb.load((kt + 1) * BK, rb);
+      load(kt + 1);
     }
-    const float* a_s = smem + cur * (FA + FB);
-    const float* b_s = a_s + FA;
+    const float* a_s = smem + cur * (FAT + FB) + aimg * FA;
+    const float* b_s = smem + cur * (FAT + FB) + FAT;
 #pragma unroll
     for (int g = 0; g < BK / 8; ++g) {
-      const float4 a0 = Img<LA::IMG, BK>::frag(a_s, ra0, g, h);
-      const float4 a1 = Img<LA::IMG, BK>::frag(a_s, ra1, g, h);
+      float4 fa[IM];
+#pragma unroll
+      for (int i = 0; i < IM; ++i) fa[i] = Img<LA::IMG, BK>::frag(a_s, rA[i], g, h);
       const float4 b0 = Img<LB::IMG, BK>::frag(b_s, rb0, g, h);
       const float4 b1 = Img<LB::IMG, BK>::frag(b_s, rb1, g, h);
-#define MDEMI_STEP(X)                                                                  \
-  acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.X, b0.X, acc[0][0], 0, 0, 0); \
-  acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.X, b1.X, acc[0][1], 0, 0, 0); \
-  acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.X, b0.X, acc[1][0], 0, 0, 0); \
-  acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.X, b1.X, acc[1][1], 0, 0, 0);
+#define MDEMI_STEP(X)                                                                        \
+  _Pragma("unroll") for (int i = 0; i < IM; ++i) {                                           \
+    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].X, b0.X, acc[i][0], 0, 0, 0);     \
+    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].X, b1.X, acc[i][1], 0, 0, 0);     \
+  }
       MDEMI_STEP(x) MDEMI_STEP(y) MDEMI_STEP(z) MDEMI_STEP(w)
 #undef MDEMI_STEP
     }
@@ -111,29 +133,28 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
     } else {
       if (more) {
         if (NBUF == 1) __syncthreads();  // everyone done reading before overwrite
-        float* dst = smem + (NBUF == 1 ? 0 : (cur ^ 1)) * (FA + FB);
-        LA::store(dst, t, ra);
-        LB::store(dst + FA, t, rb);
-        acc_rsum();
+        stage(smem + (NBUF == 1 ? 0 : (cur ^ 1)) * (FAT + FB));
       }
       __syncthreads();
       if (NBUF == 2) cur ^= 1;
     }
   }
-  if (CAN_RSUM && do_rsum) {  // reduce the 8 k-row groups (t >> 5) through LDS
+  if (CAN_RSUM && do_rsum) {  // reduce the 8 k-row groups (t >> 5) of each A image through LDS
     if (!PREF) __syncthreads();
     float4* red = reinterpret_cast<float4*>(smem);
-    red[t] = rsum;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) red[a * 256 + t] = rsum[a];
     __syncthreads();
-    if (t < 32) {
-      float4 s4 = red[t];
+    if (t < 32 * NA) {
+      const int a = t >> 5, tt = t & 31;
+      float4 s4 = red[a * 256 + tt];
 #pragma unroll
       for (int g = 1; g < 8; ++g) {
-        const float4 o = red[t + 32 * g];
+        const float4 o = red[a * 256 + tt + 32 * g];
         s4.x += o.x; s4.y += o.y; s4.z += o.z; s4.w += o.w;
       }
       float* dst = p.rowsum + (p.split > 1 ? (int64_t)sidx * p.M : 0);
-      const int i = bm + 4 * t;
+      const int i = bm + 128 * a + 4 * tt;
       if (i + 0 < p.M) dst[i + 0] = s4.x;
       if (i + 1 < p.M) dst[i + 1] = s4.y;
       if (i + 2 < p.M) dst[i + 2] = s4.z;
@@ -141,6 +162,8 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
     }
   }
 
+#define EP_IM IM
+#define EP_WTM WTM
 #include "gemm_epilogue.inc"
 }
 
@@ -152,6 +175,8 @@ static KernelFn pick_variant(int v) {
     case 3: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, true, 2>;
     case 4: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 1, true, true, 2>;
     case 5: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, false, 2>;
+    case 6: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 1, true, true, 2, 256>;
+    case 7: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 2, 256>;
     default: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 2>;
   }
 }

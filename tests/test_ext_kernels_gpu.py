@@ -409,3 +409,45 @@ def test_gemm_two_level_batch(mf, prec):
     tol = 1e-5 if prec == "fp32" else 2e-2
     assert torch.isfinite(C).all()
     close(C, ref, rtol=tol)
+
+
+@pytest.mark.parametrize("kind", ["kk", "kmn", "mnmn_rowsum", "conv"])
+def test_gemm_f32_variants_bit_identical(mf, kind):
+    """Every fp32 pipelining variant (incl. the 256-row tiles 6 and 7, which the autotuner may
+    pick per shape) adds each output's products in the same order: results are bit-identical,
+    so the tuner's choice never changes a number.  Shapes straddle tile edges (M = 300)."""
+    from mdemi import _lib as L
+    lib = L.load()
+    M, N, K = 300, 136, 200
+    outs = []
+    for v in range(8):
+        lib.mdemi_gemm_set_variant(v, 8)
+        try:
+            if kind == "kk":
+                A, B = rnd(M, K, seed=70).float().to(DEV), rnd(N, K, seed=71).float().to(DEV)
+                C = torch.empty(M, N, device=DEV)
+                mf.gemm(A, B, C, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG, split_k=1)
+                outs.append((C.clone(),))
+            elif kind == "kmn":
+                A, B = rnd(M, K, seed=72).float().to(DEV), rnd(K, N, seed=73).float().to(DEV)
+                C = torch.empty(M, N, device=DEV)
+                mf.gemm(A, B, C, M, N, K, lda=K, ldb=N, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG, split_k=3)
+                outs.append((C.clone(),))
+            elif kind == "mnmn_rowsum":  # weight-gradient form with the fused bias-gradient row sums
+                A, B = rnd(K * 8, M, seed=74).float().to(DEV), rnd(K * 8, N, seed=75).float().to(DEV)
+                C, rs = torch.empty(M, N, device=DEV), torch.empty(M, device=DEV)
+                mf.gemm(A, B, C, M, N, K * 8, lda=M, ldb=N, ldc=N, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+                        rowsum_a=rs)
+                outs.append((C.clone(), rs.clone()))
+            else:
+                x = rnd(2, 13, 17, 20, seed=76).float().to(DEV)
+                w = rnd(24, 20, 3, 3, seed=77).float().to(DEV)
+                outs.append((mf.conv2d_nhwc(x, w, None, stride=1, pad=1).clone(),))
+            torch.cuda.synchronize()
+        finally:
+            lib.mdemi_gemm_set_variant(-1, 8)
+    for v in range(1, 8):
+        for a, b in zip(outs[0], outs[v]):
+            assert torch.equal(a, b), (kind, v, (a - b).abs().max().item())
+    if kind == "kk":
+        close(outs[0][0], A.double().cpu() @ B.double().cpu().T, rtol=1e-5)
