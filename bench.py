@@ -188,44 +188,60 @@ def _gemm_alg_bytes(A, B, M, N, K, kw):
 
 
 class _HbmTimers:
-    """HIP events around the bin head's forward and backward sweeps (mdemi_binhead_nhwc_fwd /
-    _bwd, SURVEY §8d's HBM-bound row) during the instrumented step; achieved GB/s from their
-    algorithmic bytes: fwd reads the logits and writes pred + the (max, sum) row stats,
-    4*B*HW*(K+3) B; bwd reads logits, pred, stats and dpred and writes dlogits,
-    4*B*HW*(2K+4) B."""
+    """HIP events around the memory-heavy fused ops during the instrumented step, with their
+    algorithmic bytes -> achieved GB/s against the 8 TB/s HBM peak:
+      binhead_nhwc_fwd/bwd (SURVEY §8d's HBM-bound row): fwd reads the logits and writes
+        pred + the (max, sum) row stats, 4*B*HW*(K+3) B; bwd reads logits, pred, stats and
+        dpred and writes dlogits, 4*B*HW*(2K+4) B;
+      winattn_fwd/bwd (fused shifted-window attention): fwd reads q, k, v and
+        writes out, 16*C B per token; bwd reads q, k, v, out, dout and writes dq, dk, dv,
+        32*C B per token (the window's MFMA work rides on the same pass).
+    The window covers the autograd Function (its small allocations and pad fills too)."""
 
     def __init__(self, mf):
-        self.cls = mf._BinHeadNHWCFn
-        self.orig = (self.cls.forward, self.cls.backward)
-        self.recs = {"binhead_nhwc_fwd": [], "binhead_nhwc_bwd": []}
-        f0, b0 = self.orig
-
-        def sizes(logits):
+        def bh_sizes(logits):
             b, k = logits.shape[0], logits.shape[-1]
             return b, logits[0].numel() // k, k
 
-        def fwd(ctx, logits, centers):
+        def bh_fwd(args, ctx):
+            b, hw, k = bh_sizes(args[0])
+            return 4.0 * b * hw * (k + 3)
+
+        def bh_bwd(args, ctx):
+            b, hw, k = bh_sizes(ctx.saved_tensors[0])
+            return 4.0 * b * hw * (2 * k + 4)
+
+        def wa_fwd(args, ctx):
+            B, H, W, _, _, _, _, C, _ = args[5]
+            return 16.0 * C * B * H * W
+
+        def wa_bwd(args, ctx):
+            B, H, W, _, _, _, _, C, _ = ctx.geom
+            return 32.0 * C * B * H * W
+
+        self.specs = [(mf._BinHeadNHWCFn, "binhead_nhwc", bh_fwd, bh_bwd),
+                      (mf._WindowAttnFn, "winattn", wa_fwd, wa_bwd)]
+        self.orig = [(cls, cls.forward, cls.backward) for cls, _, _, _ in self.specs]
+        self.recs = {}
+        for cls, name, fb, bb in self.specs:
+            self.recs[name + "_fwd"], self.recs[name + "_bwd"] = [], []
+            cls.forward = staticmethod(self._wrap(cls.forward, fb, self.recs[name + "_fwd"], fwd=True))
+            cls.backward = staticmethod(self._wrap(cls.backward, bb, self.recs[name + "_bwd"], fwd=False))
+
+    @staticmethod
+    def _wrap(fn, nbytes, recs, fwd):
+        def timed(ctx, *args):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(torch.cuda.current_stream())
-            out = f0(ctx, logits, centers)
+            out = fn(ctx, *args)
             e.record(torch.cuda.current_stream())
-            b, hw, k = sizes(logits)
-            self.recs["binhead_nhwc_fwd"].append((4.0 * b * hw * (k + 3), s, e))
+            recs.append((nbytes(args, ctx), s, e))
             return out
-
-        def bwd(ctx, dpred):
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record(torch.cuda.current_stream())
-            out = b0(ctx, dpred)
-            e.record(torch.cuda.current_stream())
-            b, hw, k = sizes(ctx.saved_tensors[0])
-            self.recs["binhead_nhwc_bwd"].append((4.0 * b * hw * (2 * k + 4), s, e))
-            return out
-
-        self.cls.forward, self.cls.backward = staticmethod(fwd), staticmethod(bwd)
+        return timed
 
     def restore(self):
-        self.cls.forward, self.cls.backward = staticmethod(self.orig[0]), staticmethod(self.orig[1])
+        for cls, f, b in self.orig:
+            cls.forward, cls.backward = staticmethod(f), staticmethod(b)
 
     def summary(self):
         out = {}
