@@ -27,6 +27,26 @@ def closed_form_fill(state_dict, seed=0.0, scale=0.05):
     return off
 
 
+def rng_fill(state_dict, seed=0, scale=0.05):
+    """Well-conditioned alternative to closed_form_fill (full-rank Gaussian weights): entry k
+    of the floating state_dict entries, in state_dict order, gets
+        w = scale * rng_array(shape, seed * 100003 + k)
+    (1 + that for 1-D ``*weight`` entries and running_var).  The closed-form sinusoid makes
+    every weight matrix rank 2, which deep BatchNorm/LayerNorm stacks turn into fp32
+    round-off amplifiers; tests/golden/make_golden_oda2.py uses this fill."""
+    k = 0
+    with torch.no_grad():
+        for name, t in state_dict.items():
+            if not torch.is_floating_point(t):
+                continue
+            vals = scale * torch.from_numpy(rng_array(tuple(t.shape), int(seed) * 100003 + k)).double()
+            if (t.dim() == 1 and name.endswith("weight")) or name.endswith("running_var"):
+                vals = 1.0 + vals
+            t.copy_(vals.to(t.dtype))
+            k += 1
+    return k
+
+
 def rng_array(shape, seed=0):
     g = np.random.Generator(np.random.PCG64(seed))
     return g.standard_normal(size=shape).astype(np.float32)

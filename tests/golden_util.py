@@ -8,7 +8,7 @@ import numpy as np
 import torch
 
 from oracle.newcrfs import relative_position_index
-from oracle.weights import closed_form_fill, rng_array
+from oracle.weights import closed_form_fill, rng_array, rng_fill
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -19,6 +19,7 @@ class Golden:
         self.d = np.load(os.path.join(GOLDEN, name + ".npz"))
         self.spec = json.loads(str(self.d["spec"]))
         self.fill = tuple(float(x) for x in self.d["fill"])
+        self.fill_mode = str(self.d["fillmode"]) if "fillmode" in self.d else "closed_form"
 
     def keys(self, prefix):
         return [k[len(prefix):] for k in self.d.keys() if k.startswith(prefix)]
@@ -33,7 +34,10 @@ class Golden:
                 P[name] = relative_position_index(int(round(shape[0] ** 0.5)))
             else:
                 P[name] = torch.zeros(shape, dtype=torch.int64)
-        closed_form_fill(P, seed=self.fill[0], scale=self.fill[1])
+        if self.fill_mode == "rng":
+            rng_fill(P, seed=int(self.fill[0]), scale=self.fill[1])
+        else:
+            closed_form_fill(P, seed=self.fill[0], scale=self.fill[1])
         for k, v in P.items():
             if torch.is_floating_point(v):
                 P[k] = v.to(dtype)
