@@ -557,10 +557,7 @@ def main():
         H, W = args.height or wl["h"], args.width or wl["w"]
     B = args.batch or int(opt["dataloader"]["batch_size"])
     precision = args.precision or wl.get("precision", "fp32")
-    graph = args.graph or wl.get("graph", False)
-    if graph and world > 1:
-        print("bench: the hipGraph-captured step is single-GPU in this build; running eagerly", file=sys.stderr)
-        graph = False
+    graph = args.graph or wl.get("graph", False)  # data parallel too: the RCCL all-reduces are in the graph
 
     res = measure(args, opt, key, H, W, B, rank, world, device, with_roofline=not args.no_roofline,
                   precision=precision, graph=graph)

@@ -353,7 +353,8 @@ int mdemi_rowscale_add(const float* a, const float* b, const float* scale, float
 /* ------------------------------------------------------------------------ */
 typedef struct mdemi_tensor_ref {
   float* param; float* grad; float* exp_avg; float* exp_avg_sq;
-  int64_t numel; int32_t group; int32_t _pad;
+  int64_t numel; int32_t group;
+  int32_t step_slot;  /* index of this parameter's counter in tensor_steps (below) */
 } mdemi_tensor_ref;
 
 typedef struct mdemi_adamw_group {
@@ -374,22 +375,28 @@ int mdemi_grad_sumsq(const mdemi_tensor_ref* tensors_dev, int32_t ntensors, int6
  * groups_host: up to 4 parameter groups (host memory, passed by value).
  * step: 1-based step count for bias correction.  max_norm <= 0 disables the
  * clip; otherwise grads are scaled by min(1, max_norm / (sqrt(sumsq)+1e-6)),
- * as torch.nn.utils.clip_grad_norm_ does, without a host round trip. */
+ * as torch.nn.utils.clip_grad_norm_ does, without a host round trip.
+ * tensor_steps (device, optional): per-parameter step counters, torch's
+ * state[p]["step"] -- a parameter whose gradient first appears late has its own
+ * count.  When given, parameter t's bias corrections use
+ * tensor_steps[t.step_slot] + 1 (and `step` is ignored), and a trailing kernel
+ * increments tensor_steps[t.step_slot] for every tensor in the table. */
 int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                      const mdemi_adamw_group* groups_host, int32_t ngroups,
-                     const float* sumsq, float max_norm, int32_t step, int64_t nitems,
-                     void* workspace, void* stream);
+                     const float* sumsq, float max_norm, int32_t step, int32_t* tensor_steps,
+                     int64_t nitems, void* workspace, void* stream);
 /* Capturable form (a hipGraph-captured train step): the hyperparameters come
  * from device memory.  sched_dev is a [nsteps][ngroups] table of
  * mdemi_adamw_group entries -- e.g. the OneCycle lr / beta1 of every optimizer step --
- * *step_dev the number of steps already taken: the update uses row
- * min(*step_dev, nsteps - 1) and bias corrections for step *step_dev + 1, then a
- * trailing one-thread kernel increments *step_dev.  Same numerics as
- * mdemi_adamw_step. */
+ * *step_dev the number of optimizer steps already taken: the update uses row
+ * min(*step_dev, nsteps - 1) and bias corrections for step *step_dev + 1 (or, with
+ * tensor_steps, tensor_steps[t.step_slot] + 1 per parameter), then a trailing
+ * kernel increments *step_dev (and the per-parameter counters).  Same numerics
+ * as mdemi_adamw_step. */
 int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                          const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
-                         int32_t* step_dev, const float* sumsq, float max_norm, int64_t nitems,
-                         void* workspace, void* stream);
+                         int32_t* step_dev, int32_t* tensor_steps, const float* sumsq, float max_norm,
+                         int64_t nitems, void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

@@ -214,6 +214,47 @@ int mdemi_augment(const uint8_t* rgb, const uint16_t* depth, int32_t B, int32_t 
                   int32_t nyu_mask, int32_t nearest_generic, int32_t train, float saving_factor, float clip_depth,
                   float* image, float* depth_out, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* ODA2 ordered-swin2 (model/ODA2)                          */
+/* ------------------------------------------------------------------------ */
+/* Window shuffle of PreNormOrderedSwinSA (oda2_red_order_swin2_decoder.py:  */
+/* 83-85,103,126-131): roll by -shift + window_partition as one gather       */
+/* (inverse = 0): dst row r = ((n*nWh + wy)*nWw + wx)*ws^2 + ty*ws + tx       */
+/* takes src[n][(wy*ws+ty+shift) % H][(wx*ws+tx+shift) % W]; inverse = 1 is  */
+/* the scatter back (window_reverse + roll by +shift), optionally + add (the */
+/* residual `out + identity`, natural layout).  H, W multiples of ws.         */
+int mdemi_window_shuffle(const float* src, float* dst, const float* add, int32_t N, int32_t H, int32_t W,
+                         int32_t C, int32_t ws, int32_t shift, int32_t inverse, void* stream);
+/* the same gather for the int32 depth-index map [N][H][W] (:85,88) */
+int mdemi_window_shuffle_i32(const int32_t* src, int32_t* dst, int32_t N, int32_t H, int32_t W, int32_t ws,
+                             int32_t shift, void* stream);
+/* Ordered window softmax (:87-92,116-119): S, P are [nwin][heads][T][T]     */
+/* (T = ws^2 = 64 or 256), idx the window-major depth indices [nwin][T],     */
+/* table the depth_embedding [2*num_emb-1][heads] (NULL: bias_type "none").  */
+/*   P[w][h][i][j] = softmax_j(scale*S + table[idx_i - idx_j + num_emb-1][h]) */
+/* S == P is allowed.  Backward: dS = scale * P o (dP - rowsum(P o dP)) and, */
+/* when d_table != NULL, d_table[k][h] = sum of P o (dP - ...) over the     */
+/* entries whose relative index is k (overwritten).                          */
+int mdemi_ordered_softmax_fwd(const float* S, float* P, const int32_t* idx, const float* table, int32_t nwin,
+                              int32_t heads, int32_t T, int32_t num_emb, float scale, void* stream);
+size_t mdemi_ordered_softmax_bwd_workspace_size(int32_t nwin, int32_t heads, int32_t num_emb);
+int mdemi_ordered_softmax_bwd(const float* P, const float* dP, float* dS, const int32_t* idx, float* d_table,
+                              int32_t nwin, int32_t heads, int32_t T, int32_t num_emb, float scale, void* workspace,
+                              void* stream);
+/* nn.GLU(dim=-1) (oda2_red_order_reg_decoder.py:61,78): x [M][2F] ->        */
+/* y [M][F] = x[:, :F] * sigmoid(x[:, F:]); bwd writes dx [M][2F].  F % 4 == 0 */
+int mdemi_glu_fwd(const float* x, float* y, int64_t M, int32_t F, void* stream);
+int mdemi_glu_bwd(const float* x, const float* dy, float* dx, int64_t M, int32_t F, void* stream);
+/* Replicate padding / cropping as one clamp-gather over NHWC (the reference */
+/* pads with F.pad(mode="replicate"): oda2_swin_transformer.py:258,327,491,  */
+/* and the depthwise conv's padding_mode, oda2_red_order_reg_decoder.py:65): */
+/*   y[n][oy][ox] = x[n][clamp(oy-pt, 0, H-1)][clamp(ox-pl, 0, W-1)], y is   */
+/* [N][OH][OW][C].  inverse = 1 is the adjoint: x is the [N][OH][OW][C]       */
+/* gradient, y the [N][H][W][C] sum over the positions that clamp to each   */
+/* pixel.  An NCHW image is the NHWC map [N*C][H][W][1].                      */
+int mdemi_pad_replicate(const float* x, float* y, int32_t N, int32_t H, int32_t W, int32_t C, int32_t OH,
+                        int32_t OW, int32_t pt, int32_t pl, int32_t inverse, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

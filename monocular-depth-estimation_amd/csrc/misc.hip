@@ -166,11 +166,13 @@ __device__ __forceinline__ float clip_coef(const float* sumsq, float max_norm) {
 __global__ __launch_bounds__(OPT_THREADS) void adamw_kernel(const mdemi_tensor_ref* __restrict__ tl,
                                                             const int* __restrict__ chunk_tensor,
                                                             const int* __restrict__ chunk_index, AdamGroups groups,
-                                                            const float* __restrict__ sumsq, float max_norm, int step) {
+                                                            const float* __restrict__ sumsq, float max_norm, int step,
+                                                            const int* __restrict__ tensor_steps) {
   const int item = blockIdx.x;
   const mdemi_tensor_ref t = tl[chunk_tensor[item]];
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
-  adamw_item(t, groups.g[t.group], clip_coef(sumsq, max_norm), (float)step, beg, min(t.numel, beg + OPT_CHUNK));
+  const int s = tensor_steps ? tensor_steps[t.step_slot] + 1 : step;
+  adamw_item(t, groups.g[t.group], clip_coef(sumsq, max_norm), (float)s, beg, min(t.numel, beg + OPT_CHUNK));
 }
 
 // capturable form: hyperparameters of step s (= *step_dev, steps already taken)
@@ -181,16 +183,25 @@ __global__ __launch_bounds__(OPT_THREADS) void adamw_dev_kernel(const mdemi_tens
                                                                 const mdemi_adamw_group* __restrict__ sched,
                                                                 int nsteps, int ngroups,
                                                                 const int* __restrict__ step_dev,
+                                                                const int* __restrict__ tensor_steps,
                                                                 const float* __restrict__ sumsq, float max_norm) {
   const int item = blockIdx.x;
   const mdemi_tensor_ref t = tl[chunk_tensor[item]];
   const int s = step_dev[0];
   const mdemi_adamw_group gp = sched[(int64_t)min(s, nsteps - 1) * ngroups + t.group];
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
-  adamw_item(t, gp, clip_coef(sumsq, max_norm), (float)(s + 1), beg, min(t.numel, beg + OPT_CHUNK));
+  const int bc = tensor_steps ? tensor_steps[t.step_slot] + 1 : s + 1;
+  adamw_item(t, gp, clip_coef(sumsq, max_norm), (float)bc, beg, min(t.numel, beg + OPT_CHUNK));
 }
 
-__global__ void step_tick_kernel(int* step_dev) { step_dev[0] += 1; }
+// after the update: advance the optimizer's step counter and/or every listed
+// parameter's own counter (torch's state[p]["step"] += 1 for params with a grad)
+__global__ __launch_bounds__(256) void step_tick_kernel(int* step_dev, const mdemi_tensor_ref* __restrict__ tl, int nt,
+                                                        int* tensor_steps) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (step_dev && i == 0) step_dev[0] += 1;
+  if (tensor_steps && i < nt) tensor_steps[tl[i].step_slot] += 1;
+}
 
 }  // namespace mdemi
 
@@ -257,24 +268,29 @@ extern "C" int mdemi_grad_sumsq(const mdemi_tensor_ref* tensors_dev, int32_t nte
 
 extern "C" int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                                 const mdemi_adamw_group* groups_host, int32_t ngroups, const float* sumsq,
-                                float max_norm, int32_t step, int64_t nitems, void* workspace, void* stream) {
-  MDEMI_REQUIRE(tensors_dev && ntensors > 0 && groups_host && ngroups > 0 && ngroups <= 4 && step >= 1 && nitems > 0 &&
-                    workspace,
+                                float max_norm, int32_t step, int32_t* tensor_steps, int64_t nitems, void* workspace,
+                                void* stream) {
+  MDEMI_REQUIRE(tensors_dev && ntensors > 0 && groups_host && ngroups > 0 && ngroups <= 4 &&
+                    (step >= 1 || tensor_steps) && nitems > 0 && workspace,
                 "adamw_step: bad args");
   AdamGroups g;
   for (int i = 0; i < ngroups; ++i) g.g[i] = groups_host[i];
   for (int i = ngroups; i < 4; ++i) g.g[i] = groups_host[0];
   const int* ct = (const int*)workspace;
   const int* ci = ct + nitems;
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, (hipStream_t)stream, tensors_dev, ct,
-                     ci, g, sumsq, max_norm, step);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, st, tensors_dev, ct, ci, g, sumsq,
+                     max_norm, step, (const int*)tensor_steps);
+  if (tensor_steps)
+    hipLaunchKernelGGL(step_tick_kernel, dim3((unsigned)cdiv(ntensors, 256)), dim3(256), 0, st, (int*)nullptr,
+                       tensors_dev, ntensors, (int*)tensor_steps);
   return check_launch("adamw_step");
 }
 
 extern "C" int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                                     const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
-                                    int32_t* step_dev, const float* sumsq, float max_norm, int64_t nitems,
-                                    void* workspace, void* stream) {
+                                    int32_t* step_dev, int32_t* tensor_steps, const float* sumsq, float max_norm,
+                                    int64_t nitems, void* workspace, void* stream) {
   MDEMI_REQUIRE(tensors_dev && ntensors > 0 && sched_dev && nsteps > 0 && ngroups > 0 && ngroups <= 4 && step_dev &&
                     nitems > 0 && workspace,
                 "adamw_step_dev: bad args");
@@ -282,8 +298,9 @@ extern "C" int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t
   const int* ci = ct + nitems;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(adamw_dev_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, st, tensors_dev, ct, ci, sched_dev,
-                     nsteps, ngroups, (const int*)step_dev, sumsq, max_norm);
-  hipLaunchKernelGGL(step_tick_kernel, dim3(1), dim3(1), 0, st, (int*)step_dev);
+                     nsteps, ngroups, (const int*)step_dev, (const int*)tensor_steps, sumsq, max_norm);
+  hipLaunchKernelGGL(step_tick_kernel, dim3((unsigned)cdiv(ntensors, 256)), dim3(256), 0, st, (int*)step_dev,
+                     tensors_dev, ntensors, (int*)tensor_steps);
   return check_launch("adamw_step_dev");
 }
 

@@ -89,7 +89,7 @@ class WinAttnDesc(ctypes.Structure):
 
 class TensorRef(ctypes.Structure):
     _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp),
-                ("numel", i64), ("group", i32), ("_pad", i32)]
+                ("numel", i64), ("group", i32), ("step_slot", i32)]
 
 
 class AdamWGroup(ctypes.Structure):
@@ -157,8 +157,8 @@ _SIGS = {
     "mdemi_multi_tensor_chunk": (ctypes.c_int, []),
     "mdemi_grad_norm_workspace_size": (sz, [i32]),
     "mdemi_grad_sumsq": (ctypes.c_int, [vp, i32, i64, vp, vp, vp]),
-    "mdemi_adamw_step": (ctypes.c_int, [vp, i32, ctypes.POINTER(AdamWGroup), i32, vp, f32, i32, i64, vp, vp]),
-    "mdemi_adamw_step_dev": (ctypes.c_int, [vp, i32, vp, i32, i32, vp, vp, f32, i64, vp, vp]),
+    "mdemi_adamw_step": (ctypes.c_int, [vp, i32, ctypes.POINTER(AdamWGroup), i32, vp, f32, i32, vp, i64, vp, vp]),
+    "mdemi_adamw_step_dev": (ctypes.c_int, [vp, i32, vp, i32, i32, vp, vp, vp, f32, i64, vp, vp]),
     # ---- include/mdemi_ext.h ----
     "mdemi_dwconv_fwd": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mdemi_dwconv_bwd_workspace_size": (sz, [i32, i32, i32, i32, i32]),
@@ -193,6 +193,14 @@ _SIGS = {
     "mdemi_conv_weight_layout": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
     "mdemi_augment": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32,
                                      f32, f32, vp, vp, vp]),
+    "mdemi_window_shuffle": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "mdemi_window_shuffle_i32": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
+    "mdemi_ordered_softmax_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, f32, vp]),
+    "mdemi_ordered_softmax_bwd_workspace_size": (sz, [i32, i32, i32]),
+    "mdemi_ordered_softmax_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp, vp]),
+    "mdemi_glu_fwd": (ctypes.c_int, [vp, vp, i64, i32, vp]),
+    "mdemi_glu_bwd": (ctypes.c_int, [vp, vp, vp, i64, i32, vp]),
+    "mdemi_pad_replicate": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
 }
 
 _lib = None
@@ -255,10 +263,18 @@ def stream() -> int:
 
 # ---- per-device scratch (the library never allocates) ----
 _ws: dict = {}
-# Every workspace buffer ever handed out stays alive: a captured hipGraph keeps
-# the raw addresses it was recorded with, so a buffer superseded by a larger one
-# (a later eager call at a bigger shape) must never return to the allocator.
+# Once a hipGraph has been captured, a workspace buffer superseded by a larger one
+# (a later eager call at a bigger shape) must never return to the allocator: the
+# graph keeps the raw addresses it was recorded with.  Before any capture,
+# superseded buffers are simply freed.
 _ws_retired: list = []
+_graph_captured = False
+
+
+def note_graph_capture() -> None:
+    """Called when a workspace is handed out during a capture (and by Trainer)."""
+    global _graph_captured
+    _graph_captured = True
 
 
 def workspace(nbytes: int, device=None, slot: int = 0) -> torch.Tensor:
@@ -268,11 +284,14 @@ def workspace(nbytes: int, device=None, slot: int = 0) -> torch.Tensor:
     key = (device.index if device.index is not None else torch.cuda.current_device(), slot)
     buf = _ws.get(key)
     nbytes = max(int(nbytes), 256)
+    capturing = torch.cuda.is_current_stream_capturing()
+    if capturing:
+        note_graph_capture()
     if buf is None or buf.numel() < nbytes:
-        if torch.cuda.is_current_stream_capturing():
+        if capturing:
             raise RuntimeError(f"mdemi: workspace slot {slot} must grow to {nbytes} bytes during hipGraph capture; "
                                "run the captured step eagerly first (warm-up) so every workspace is sized")
-        if buf is not None:
+        if buf is not None and _graph_captured:
             _ws_retired.append(buf)
         buf = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=device)
         _ws[key] = buf

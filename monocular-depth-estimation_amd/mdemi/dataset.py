@@ -4,7 +4,8 @@ The reference's ``DepthDataset.__getitem__`` (:166-236) decodes one sample with 
 then crops, rotates, flips, colour-augments and normalises it in numpy on a DataLoader
 worker.  Here the worker only decodes the files (``DepthDataset.__getitem__`` returns the
 raw uint8 RGB and uint16 depth, KITTI already KB-cropped, :197-206), the batch is stacked
-into pinned host memory, and ``GpuSampleTransform`` runs everything after decoding as one
+(``collate_raw``; pass ``DataLoader(pin_memory=True)`` so the main process's pin thread, not a
+forked worker, pins it), and ``GpuSampleTransform`` runs everything after decoding as one
 libmdemi sweep over the batch (``mdemi_augment``, csrc/augment.hip): the NYU valid-region
 mask (:213-217), Pillow's rotate (:219-222), /255 and /saving_factor (:224-228),
 random_crop (:238-248), the flip and colour augmentation (:250-280), hide_depth
@@ -156,8 +157,10 @@ class DepthDataset(torch.utils.data.Dataset):
                                   self.clip_depth, self.height_drop, self.width_drop, self.drop_edge)
 
 
-def collate_raw(samples: List[Dict], pin: bool = True) -> Dict:
-    """Stack decoded samples into (B,H,W,3) uint8 / (B,H,W) uint16 host tensors."""
+def collate_raw(samples: List[Dict], pin: bool = False) -> Dict:
+    """Stack decoded samples into (B,H,W,3) uint8 / (B,H,W) uint16 host tensors.
+    pin=True pins them here -- only in a process that may initialise HIP (not a forked
+    DataLoader worker: use DataLoader(collate_fn=collate_raw, pin_memory=True) there)."""
     img = torch.from_numpy(np.stack([s["image"] for s in samples]))
     dep = torch.from_numpy(np.stack([s["depth"] for s in samples]).view(np.int16))
     if pin and torch.cuda.is_available():

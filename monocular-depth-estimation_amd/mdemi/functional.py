@@ -1907,3 +1907,247 @@ class _ResizeConcatFn(torch.autograd.Function):
 
 def resize_concat(pieces, size, align_corners=True):
     return _ResizeConcatFn.apply(tuple(size), align_corners, *pieces)
+
+
+# ==========================================================================
+# ODA2 ordered-swin2 ops (include/mdemi_ext.h, csrc/oda2.hip)
+# ==========================================================================
+
+
+class _PadReplicateFn(torch.autograd.Function):
+    """Clamp-gather of an NHWC map to (OH, OW) with top/left offsets (pt, pl): replicate
+    padding on any side and/or cropping.  Backward folds the gradient onto the source."""
+
+    @staticmethod
+    def forward(ctx, x, oh, ow, pt, pl):
+        _require_cuda(x)
+        x = _c(x)
+        n, h, w, c = x.shape
+        y = torch.empty(n, oh, ow, c, device=x.device, dtype=torch.float32)
+        L.call("mdemi_pad_replicate", x.data_ptr(), y.data_ptr(), n, h, w, c, oh, ow, pt, pl, 0, L.stream())
+        ctx.cfg = (n, h, w, c, oh, ow, pt, pl)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c, oh, ow, pt, pl = ctx.cfg
+        dy = _c(dy)
+        dx = torch.empty(n, h, w, c, device=dy.device, dtype=torch.float32)
+        L.call("mdemi_pad_replicate", dy.data_ptr(), dx.data_ptr(), n, h, w, c, oh, ow, pt, pl, 1, L.stream())
+        return dx, None, None, None, None
+
+
+def pad_replicate_nhwc(x, top=0, bottom=0, left=0, right=0):
+    """F.pad(..., mode='replicate') of an NHWC map's H / W (negative bottom/right crop)."""
+    n, h, w, c = x.shape
+    if top == bottom == left == right == 0:
+        return x
+    return _PadReplicateFn.apply(x, h + top + bottom, w + left + right, top, left)
+
+
+def replicate_rows_nchw_no_grad(img, oh, ow):
+    """Clamp-gather of an NCHW image (no gradient) as the NHWC map [N*C, H, W, 1]."""
+    _require_cuda(img)
+    img = _c(img)
+    n, c, h, w = img.shape
+    y = torch.empty(n, c, oh, ow, device=img.device, dtype=torch.float32)
+    L.call("mdemi_pad_replicate", img.data_ptr(), y.data_ptr(), n * c, h, w, 1, oh, ow, 0, 0, 0, L.stream())
+    return y
+
+
+def resize_nchw_no_grad(img, oh, ow, align_corners=True):
+    """Bilinear resize of an NCHW image that needs no gradient (the network input): the NHWC
+    sweep over the [N*C, H, W, 1] view."""
+    _require_cuda(img)
+    img = _c(img)
+    n, c, h, w = img.shape
+    y = torch.empty(n, c, oh, ow, device=img.device, dtype=torch.float32)
+    L.call("mdemi_bilinear_fwd", img.data_ptr(), y.data_ptr(), n * c, h, w, 1, oh, ow, int(align_corners), 0.0, 0.0,
+           1, 1, L.stream())
+    return y
+
+
+class _WindowShuffleFn(torch.autograd.Function):
+    """roll(-shift) + window_partition of an NHWC map into window-major rows [N*H*W, C]
+    (oda2_red_order_swin2_decoder.py:83-85,103); backward is the scatter back."""
+
+    @staticmethod
+    def forward(ctx, x, ws, shift):
+        _require_cuda(x)
+        x = _c(x)
+        n, h, w, c = x.shape
+        y = torch.empty(n * h * w, c, device=x.device, dtype=torch.float32)
+        L.call("mdemi_window_shuffle", x.data_ptr(), y.data_ptr(), None, n, h, w, c, ws, shift, 0, L.stream())
+        ctx.cfg = (n, h, w, c, ws, shift)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c, ws, shift = ctx.cfg
+        dy = _c(dy)
+        dx = torch.empty(n, h, w, c, device=dy.device, dtype=torch.float32)
+        L.call("mdemi_window_shuffle", dy.data_ptr(), dx.data_ptr(), None, n, h, w, c, ws, shift, 1, L.stream())
+        return dx, None, None
+
+
+class _WindowUnshuffleAddFn(torch.autograd.Function):
+    """window_reverse + roll(+shift) of window-major rows back to NHWC, plus a residual in
+    the natural layout (:126-131 `out + identity`)."""
+
+    @staticmethod
+    def forward(ctx, y_win, identity, ws, shift):
+        _require_cuda(y_win, identity)
+        y_win, identity = _c(y_win), _c(identity)
+        n, h, w, c = identity.shape
+        out = torch.empty_like(identity)
+        L.call("mdemi_window_shuffle", y_win.data_ptr(), out.data_ptr(), identity.data_ptr(), n, h, w, c, ws, shift,
+               1, L.stream())
+        ctx.cfg = (n, h, w, c, ws, shift)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c, ws, shift = ctx.cfg
+        dy = _c(dy)
+        dwin = torch.empty(n * h * w, c, device=dy.device, dtype=torch.float32)
+        L.call("mdemi_window_shuffle", dy.data_ptr(), dwin.data_ptr(), None, n, h, w, c, ws, shift, 0, L.stream())
+        return dwin, dy, None, None
+
+
+def window_shuffle(x_nhwc, ws, shift):
+    return _WindowShuffleFn.apply(x_nhwc, ws, shift)
+
+
+def window_unshuffle_add(y_win, identity_nhwc, ws, shift):
+    return _WindowUnshuffleAddFn.apply(y_win, identity_nhwc, ws, shift)
+
+
+def window_indices(idx_nhw, ws, shift):
+    """int32 depth-index map [N, H, W] -> window-major [N*H*W] (rolled by -shift)."""
+    idx = idx_nhw.to(torch.int32).contiguous()
+    n, h, w = idx.shape
+    out = torch.empty(n * h * w, device=idx.device, dtype=torch.int32)
+    L.call("mdemi_window_shuffle_i32", idx.data_ptr(), out.data_ptr(), n, h, w, ws, shift, L.stream())
+    return out
+
+
+class _OrderedWindowAttnFn(torch.autograd.Function):
+    """Per window and head: P = softmax(scale * drop(Q K^T) + E[idx_i - idx_j + n-1, h]),
+    O = P V (oda2_red_order_swin2_decoder.py:111-122; attention dropout acts on the scaled
+    scores before the bias, :117).  q/k/v are column slices [0,d) / [d,2d) / [2d,3d) of one
+    window-major [nwin*T, 3d] buffer; QK^T, PV and their gradients are batched MFMA GEMMs
+    (batch = (window, head)); the biased softmax and its backward (with the embedding
+    gradient) are one sweep each.  Returns (O [nwin*T, d], P [nwin, heads, T, T])."""
+
+    @staticmethod
+    def forward(ctx, qkv, idx_win, table, cfg):
+        nwin, T, heads, hd, num_emb, scale, p, seed = cfg
+        _require_cuda(qkv, table)
+        qkv = _c(qkv)
+        d = heads * hd
+        ld = 3 * d
+        dev = qkv.device
+        hs = T * T
+        S = torch.empty(nwin, heads, T, T, device=dev, dtype=torch.float32)
+        gemm(qkv, qkv, S, T, T, hd, lda=ld, ldb=ld, ldc=T, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+             batch=nwin * heads, a_bstride=T * ld, b_bstride=T * ld, c_bstride=heads * hs, a_off=0, b_off=d,
+             inner=(heads, hd, hd, hs))
+        if p > 0.0:
+            _drop(S.data_ptr(), S.data_ptr(), S.numel(), p, seed)
+        L.call("mdemi_ordered_softmax_fwd", S.data_ptr(), S.data_ptr(), L.ptr(idx_win), L.ptr(table), nwin, heads, T,
+               num_emb, float(scale), L.stream())
+        P = S
+        out = torch.empty(nwin * T, d, device=dev, dtype=torch.float32)
+        gemm(P, qkv, out, T, hd, T, lda=T, ldb=ld, ldc=d, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
+             batch=nwin * heads, a_bstride=heads * hs, b_bstride=T * ld, c_bstride=T * d, b_off=2 * d,
+             inner=(heads, hs, hd, hd))
+        ctx.save_for_backward(qkv, P, idx_win)
+        ctx.cfg = cfg
+        ctx.has_table = table is not None
+        return out, P
+
+    @staticmethod
+    def backward(ctx, dout, dP_ext):
+        qkv, P, idx_win = ctx.saved_tensors
+        nwin, T, heads, hd, num_emb, scale, p, seed = ctx.cfg
+        d = heads * hd
+        ld = 3 * d
+        hs = T * T
+        dev = qkv.device
+        dqkv = torch.empty_like(qkv)
+        dP = torch.empty_like(P)
+        if dout is not None:
+            dout = _c(dout)
+            gemm(dout, qkv, dP, T, T, hd, lda=d, ldb=ld, ldc=T, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+                 batch=nwin * heads, a_bstride=T * d, b_bstride=T * ld, c_bstride=heads * hs, b_off=2 * d,
+                 inner=(heads, hd, hd, hs))
+            gemm(P, dout, dqkv, T, hd, T, lda=T, ldb=d, ldc=ld, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+                 batch=nwin * heads, a_bstride=heads * hs, b_bstride=T * d, c_bstride=T * ld, c_off=2 * d,
+                 inner=(heads, hs, hd, hd))
+            if dP_ext is not None:
+                dP_ext = _c(dP_ext)
+                L.call("mdemi_elementwise", L.EW_ADD, dP.data_ptr(), dP_ext.data_ptr(), dP.data_ptr(), dP.numel(),
+                       0.0, 0.0, L.stream())
+        else:
+            dqkv[:, 2 * d:].zero_()
+            if dP_ext is not None:
+                _copy2d(_c(dP_ext).view(-1, T), dP.view(-1, T))
+            else:
+                dP.zero_()
+        dtab = None
+        lib = L.load()
+        if ctx.has_table and ctx.needs_input_grad[2]:
+            dtab = torch.empty(2 * num_emb - 1, heads, device=dev, dtype=torch.float32)
+            ws = L.workspace(lib.mdemi_ordered_softmax_bwd_workspace_size(nwin, heads, num_emb), dev)
+            wsp = ws.data_ptr()
+        else:
+            wsp = None
+        L.check(lib.mdemi_ordered_softmax_bwd(P.data_ptr(), dP.data_ptr(), dP.data_ptr(), L.ptr(idx_win), L.ptr(dtab),
+                                              nwin, heads, T, num_emb, float(scale), wsp, L.stream()),
+                "ordered_softmax_bwd")
+        dS = dP
+        if p > 0.0:
+            _drop(dS.data_ptr(), dS.data_ptr(), dS.numel(), p, seed)
+        # dQ = dS K ; dK = dS^T Q
+        gemm(dS, qkv, dqkv, T, hd, T, lda=T, ldb=ld, ldc=ld, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
+             batch=nwin * heads, a_bstride=heads * hs, b_bstride=T * ld, c_bstride=T * ld, b_off=d, c_off=0,
+             inner=(heads, hs, hd, hd))
+        gemm(dS, qkv, dqkv, T, hd, T, lda=T, ldb=ld, ldc=ld, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+             batch=nwin * heads, a_bstride=heads * hs, b_bstride=T * ld, c_bstride=T * ld, b_off=0, c_off=d,
+             inner=(heads, hs, hd, hd))
+        return dqkv, None, dtab, None
+
+
+def ordered_window_attention(qkv_win, idx_win, table, nwin, T, heads, hd, num_emb, scale, p=0.0, training=False):
+    p = float(p) if training else 0.0
+    seed = _draw_seed(qkv_win.device) if p > 0.0 else None
+    cfg = (nwin, T, heads, hd, int(num_emb), float(scale), p, seed)
+    return _OrderedWindowAttnFn.apply(qkv_win, idx_win, table, cfg)
+
+
+class _GluFn(torch.autograd.Function):
+    """nn.GLU(dim=-1): x[..., :F] * sigmoid(x[..., F:])."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _require_cuda(x)
+        x = _c(x)
+        F2 = x.shape[-1]
+        M = x.numel() // F2
+        y = torch.empty(*x.shape[:-1], F2 // 2, device=x.device, dtype=torch.float32)
+        L.call("mdemi_glu_fwd", x.data_ptr(), y.data_ptr(), M, F2 // 2, L.stream())
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = _c(dy)
+        F2 = x.shape[-1]
+        dx = torch.empty_like(x)
+        L.call("mdemi_glu_bwd", x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel() // F2, F2 // 2, L.stream())
+        return dx
+
+
+def glu(x):
+    return _GluFn.apply(x)

@@ -10,8 +10,14 @@ unchanged, onto this framework's objects:
   model.name            adabins        -> UnetAdaptiveBins.build(num_bins, min, max)   unet_adaptive_bins.py:126-139
                         newcrfs        -> NewCRFDepth('large07', max_depth=max)        NewCRFDepth.py:15
                         depthformer_v8 -> DepthformerV8.build(opt.model, min, max)      depthformer_v8.py:84-102
+                        oda2_red_order_swin2 -> ODA2OrderedSwin2RegModel.build(...)    oda2_red_order_swin2.py:98-118
+                           (model.use_checkpoint, default the reference's True, toggles the
+                           encoder's activation checkpointing)
   model.bn_momentum     -> every BatchNorm's momentum
-  loss.alpha/beta/per_image -> SILogLoss (+ loss.chamfer_weight x BinsChamferLoss on the bins)
+  loss.alpha/beta/per_image -> SILogLoss (+ loss.chamfer_weight x BinsChamferLoss on the bins;
+                        ODA2: loss.si_weight x the mean SILog over every output the model returns
+                        -- the head's earlier outputs get gradient from nowhere else, its
+                        depth indices are detached, :246-253)
   optimizer.lr/weight_decay/betas/eps/same_lr -> FusedAdamW; with get_1x_lr_params
                         (unet_adaptive_bins.py:111-117) and same_lr false: two groups,
                         encoder at lr/10, the rest at lr
@@ -38,7 +44,7 @@ import torch.nn as nn
 from .loss import BinsChamferLoss, SILogLoss
 from .optim import FusedAdamW, OneCycleLR
 
-MODEL_NAMES = ("adabins", "newcrfs", "depthformer_v8")
+MODEL_NAMES = ("adabins", "newcrfs", "depthformer_v8", "oda2_red_order_swin2")
 # training-split sizes behind the default steps-per-epoch: depth_dataset.py:79 reads
 # train_test_inputs/NYU/nyu_train_36k.txt (36,253 pairs), :49 KITTI/kitti_eigen_train.txt
 # (23,158); ONLINE's kitti_benchmark_train.txt is a missing blob, so KITTI's count stands in
@@ -64,6 +70,12 @@ def build_model(opt, drop_path=None):
     elif name == "depthformer_v8":
         from ..model.Depthformer import DepthformerV8
         model = DepthformerV8.build(m, dmin, dmax)
+    elif name == "oda2_red_order_swin2":
+        from ..model.ODA2 import ODA2OrderedSwin2RegModel
+        kw = {"use_checkpoint": bool(m.get("use_checkpoint", True))}
+        if drop_path is not None:
+            kw["path_drop_prob"] = drop_path
+        model = ODA2OrderedSwin2RegModel.build(m, dmin, dmax, **kw)
     else:
         raise ValueError(f"model.name {name!r} is not on this framework's path (one of {MODEL_NAMES})")
     if "bn_momentum" in m:
@@ -84,8 +96,16 @@ class TrainLoss:
                                per_image=bool(lo.get("per_image", False)), min_depth=dmin)
         self.w = float(lo.get("chamfer_weight", 0.0))
         self.chamfer = BinsChamferLoss(dmin, from_edges=(model_name == "adabins")) if self.w > 0 else None
+        self.multi = model_name == "oda2_red_order_swin2"
+        self.si_weight = float(lo.get("si_weight", 1.0))
 
     def __call__(self, out, gt):
+        if self.multi:  # (out, outs, attn): every output, each upsampled to the GT
+            outs = out[1]
+            loss = self.silog(outs[0], gt)
+            for o in outs[1:]:
+                loss = loss + self.silog(o, gt)
+            return loss * (self.si_weight / len(outs))
         pred = out[0] if isinstance(out, tuple) else out
         loss = self.silog(pred, gt)  # SILogLoss upsamples a half-resolution prediction to the GT first
         if self.chamfer is not None:
@@ -146,12 +166,17 @@ class Trainer:
     precision "bf16": every libmdemi GEMM (Linear, conv, attention products; forward and
     backward) runs with bf16 operands and fp32 accumulation -- torch.autocast's matmul
     numerics -- while master weights, optimizer state and the other kernels stay fp32.
+
     graph=True: the first two calls run eagerly (they settle GEMM autotuning, every
-    workspace and the optimizer state; gradients stay allocated), the third captures the
-    whole step -- forward, loss, backward, clip, AdamW with its schedule read on the
-    device -- into a hipGraph (torch.cuda.CUDAGraph) and replays it; every later call copies
-    its batch into the static input buffers and replays.  Each call is exactly one
-    optimizer step.  Dropout seeds are drawn on the GPU, so masks differ per replay."""
+    workspace, the optimizer state and, data-parallel, the RCCL communicator; gradients
+    stay allocated), the third captures the whole step -- forward, loss, backward, the
+    bucketed RCCL all-reduces the backward hooks launch, the 1/world scaling, clip, AdamW
+    with its schedule read on the device -- into a hipGraph (torch.cuda.CUDAGraph) and
+    replays it; every later call copies its batch into the static input buffers and
+    replays.  Data-parallel, the hooks run once, at capture: the bucket launch order is
+    recorded then and every replay issues the same collective sequence on every rank.
+    Each call is exactly one optimizer step.  Dropout seeds are drawn on the GPU, so
+    masks differ per replay."""
 
     def __init__(self, opt, model, criterion, optimizer, scheduler, ddp=None, precision="fp32", graph=False):
         tr = opt.get("train", {})
@@ -167,13 +192,12 @@ class Trainer:
         self.precision = precision
         self.graph = bool(graph)
         if self.graph:
-            if ddp is not None:
-                raise NotImplementedError("graph capture of the data-parallel step is not built (use graph=False)")
             if not getattr(optimizer, "capturable", False):
                 raise ValueError("graph=True needs FusedAdamW(capturable=True)")
             if scheduler is not None:
                 optimizer.set_schedule(scheduler.hyper_table())
         self._graph = None
+        self._graph_layout = None
         self._eager_calls = 0
 
     def train_mode(self):
@@ -197,42 +221,40 @@ class Trainer:
 
     def _graph_step(self, batches):
         from .. import functional as mf
+        if self._graph is not None and self.optimizer.layout_version != self._graph_layout:
+            # optimizer state was replaced (load_state_dict with new tensors): the captured
+            # pointer table is stale -- rebuild it with one eager step, then re-capture
+            self._graph = None
+            self._eager_calls = 1
         if self._graph is None:
-            if self._eager_calls < 2:  # warm-up: autotuning, workspaces, optimizer state
+            if self._eager_calls < 2:  # warm-up: autotuning, workspaces, optimizer state, communicator
                 self._eager_calls += 1
                 with mf.matmul_precision(self.precision):
                     return self._eager_step(batches)
             self._static = [(img.clone(), gt.clone()) for img, gt in batches]
-            self.optimizer.zero_grad(set_to_none=False)
+            self._zero_grad(set_to_none=False)
+            if self.ddp is not None:
+                torch.cuda.synchronize()  # no collective of the eager steps may still be in flight
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g), mf.matmul_precision(self.precision):
                 self._static_loss = self._body(self._static)
-            self.optimizer.step_count -= 1  # capture records the step, it does not run it
+                self._zero_grad(set_to_none=False)  # gradients keep their (captured) addresses
             self._graph = g
+            self._graph_layout = self.optimizer.layout_version
         else:
             for (si, sg), (img, gt) in zip(self._static, batches):
                 si.copy_(img, non_blocking=True)
                 sg.copy_(gt, non_blocking=True)
         self._graph.replay()
-        self.optimizer.step_count += 1  # host mirror of the device step counter
+        self.optimizer.replayed()  # host mirrors of the device step counters
         if self.scheduler is not None:
             self.scheduler.step()
         return self._static_loss
 
     def _body(self, batches):
-        """The captured step: no host synchronisation, no host-side hyperparameters."""
-        total = None
-        for img, gt in batches:
-            loss = self.criterion(self.model(img), gt)
-            if self.num_accum > 1:
-                loss = loss * (1.0 / self.num_accum)
-            loss.backward()
-            total = loss.detach() if total is None else total + loss.detach()
-        self.optimizer.step()
-        self.optimizer.zero_grad(set_to_none=False)  # gradients keep their (captured) addresses
-        return total
-
-    def _eager_step(self, batches):
+        """Micro-batches (all but the last under no_sync), the gradient exchange and the
+        optimizer update: no host synchronisation and no host-side hyperparameter in the
+        capturable case, so the same code is what a hipGraph records."""
         total = None
         for i, (img, gt) in enumerate(batches):
             last = i == len(batches) - 1
@@ -246,12 +268,19 @@ class Trainer:
         if self.ddp is not None:
             self.ddp.finish()
         self.optimizer.step()
+        return total
+
+    def _zero_grad(self, set_to_none):
+        if self.ddp is not None:
+            self.ddp.zero_grad()  # bucket views stay in place
+        else:
+            self.optimizer.zero_grad(set_to_none=set_to_none)
+
+    def _eager_step(self, batches):
+        total = self._body(batches)
         if self.scheduler is not None:
             self.scheduler.step()
-        if self.ddp is not None:
-            self.ddp.zero_grad()
-        else:
-            self.optimizer.zero_grad(set_to_none=not self.graph)
+        self._zero_grad(set_to_none=not self.graph)
         return total
 
 
@@ -264,12 +293,12 @@ class _null:
 
 
 def build_from_config(opt, device=None, world=1, steps_per_epoch=None, ddp_bucket_mb=64.0, drop_path=None,
-                      precision=None, graph=False):
+                      precision=None, graph=False, ddp=None):
     """opt (parse()'s dict) -> Trainer.  device='meta' builds every object without
-    allocating parameters (config validation); world > 1 wraps the gradients in the
-    bucketed RCCL all-reduce (needs an initialised process group).  precision
-    (default: train.precision or "fp32") and graph select the mixed-precision /
-    hipGraph-captured step (Trainer)."""
+    allocating parameters (config validation); world > 1 (or ddp=True, e.g. a world-1
+    RCCL group) wraps the gradients in the bucketed RCCL all-reduce (needs an
+    initialised process group).  precision (default: train.precision or "fp32") and
+    graph select the mixed-precision / hipGraph-captured step (Trainer)."""
     name = opt["model"]["name"]
     if device is not None and torch.device(device).type == "meta":
         with torch.device("meta"):
@@ -282,12 +311,12 @@ def build_from_config(opt, device=None, world=1, steps_per_epoch=None, ddp_bucke
     optimizer = build_optimizer(model, opt, capturable=graph)
     spe = steps_per_epoch if steps_per_epoch is not None else optimizer_steps_per_epoch(opt, world)
     scheduler = build_scheduler(optimizer, opt, spe)
-    ddp = None
-    if world > 1:
+    grad_ar = None
+    if (world > 1) if ddp is None else ddp:
         from .ddp import GradAllReduce, broadcast_parameters
         broadcast_parameters(model)
-        ddp = GradAllReduce(model, bucket_mb=ddp_bucket_mb)
+        grad_ar = GradAllReduce(model, bucket_mb=ddp_bucket_mb)
     precision = precision or opt.get("train", {}).get("precision", "fp32")
-    trainer = Trainer(opt, model, criterion, optimizer, scheduler, ddp, precision=precision, graph=graph)
+    trainer = Trainer(opt, model, criterion, optimizer, scheduler, grad_ar, precision=precision, graph=graph)
     trainer.train_mode()
     return trainer

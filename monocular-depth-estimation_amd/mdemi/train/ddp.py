@@ -35,6 +35,8 @@ import torch.distributed as dist
 
 
 class GradAllReduce:
+    SLOT_ALIGN = 64  # elements
+
     def __init__(self, model, bucket_mb: float = 64.0, group=None):
         self.group = group
         self.world = dist.get_world_size(group)
@@ -57,14 +59,15 @@ class GradAllReduce:
         self.bucket_of, self.slot = {}, {}
         self.flat = []
         for bi, b in enumerate(self.buckets):
-            n = sum(p.numel() for p in b)
-            flat = torch.zeros(n, dtype=dtype, device=dev)
-            self.flat.append(flat)
+            # every slot starts on a SLOT_ALIGN-element (256-B) boundary, so each .grad view
+            # is as aligned as a fresh allocation and the vectorised sweeps over it (the norm,
+            # AdamW) never fall back to scalar paths; the gaps are zero and stay zero
             off = 0
             for p in b:
                 self.bucket_of[p] = bi
                 self.slot[p] = (off, p.numel())
-                off += p.numel()
+                off += -(-p.numel() // self.SLOT_ALIGN) * self.SLOT_ALIGN
+            self.flat.append(torch.zeros(off, dtype=dtype, device=dev))
         self.bucket_bytes = [f.numel() * f.element_size() for f in self.flat]
         self._install_views(copy_existing=True)
         self.launch_order: list[int] = []

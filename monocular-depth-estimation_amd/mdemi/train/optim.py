@@ -16,11 +16,17 @@ class FusedAdamW:
     """torch.optim.AdamW semantics (decoupled weight decay, amsgrad=False) for fp32
     CUDA params; one gradient-norm kernel + one update kernel per step, no host sync.
 
-    capturable=True: the per-step hyperparameters (lr, betas, bias-correction step) are
-    read on the device from a schedule table (set_schedule; default: the groups' current
-    values) indexed by a device step counter, so the whole step can live in a captured
-    hipGraph (mdemi_adamw_step_dev).  The host mirror (step_count, param_groups) is
-    advanced by the caller on each replay (Trainer does)."""
+    Each parameter keeps its own step count (torch's state[p]["step"]): a parameter
+    whose gradient first appears at optimizer step k is bias-corrected as step 1 there.
+    The counts live in a device int32 array (one slot per parameter, in param_groups
+    order) that the update kernel reads and a trailing kernel advances; ``steps`` is the
+    host mirror.
+
+    capturable=True: the per-step hyperparameters (lr, betas) are read on the device
+    from a schedule table (set_schedule; default: the groups' current values) indexed by
+    a device step counter, so the whole step can live in a captured hipGraph
+    (mdemi_adamw_step_dev).  The host mirrors (step_count, steps) are advanced by the
+    caller after each replay (``replayed()``; Trainer does)."""
 
     def __init__(self, param_groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, max_grad_norm=0.0,
                  capturable=False):
@@ -43,13 +49,24 @@ class FusedAdamW:
             raise ValueError("FusedAdamW: at most 4 parameter groups")
         self.max_grad_norm = float(max_grad_norm)
         self.state = {}
-        self.step_count = 0
+        self.step_count = 0  # optimizer steps taken (the schedule position)
+        self._slot = {}
+        for p in (p for g in self.param_groups for p in g["params"]):
+            self._slot.setdefault(p, len(self._slot))
+        self.steps = [0] * len(self._slot)  # host mirror of the per-parameter step counters
+        self._steps_dev = None
         self._chunk = L.load().mdemi_multi_tensor_chunk()
         self._sumsq = None
         self.capturable = bool(capturable)
         self._sched_rows = None  # host schedule [(lr, beta1, beta2, eps, wd) per group] per step
         self._sched_dev = None
         self._step_dev = None
+        self._tbl_key = None
+        self._tbl_slots = []
+        # bumped whenever a device address the update reads may have changed (new state
+        # tensors, a rebuilt pointer table): a captured graph recorded with an older
+        # layout must be re-captured (Trainer checks)
+        self.layout_version = 0
 
     # ---- capturable schedule ----
     def set_schedule(self, rows):
@@ -58,6 +75,7 @@ class FusedAdamW:
             raise ValueError("FusedAdamW.set_schedule: one row per step, one entry per parameter group")
         self._sched_rows = [[tuple(float(v) for v in e) for e in r] for r in rows]
         self._sched_dev = None
+        self.layout_version += 1
 
     def _device_schedule(self, dev, taken):
         """taken: optimizer steps completed before the one being launched."""
@@ -69,7 +87,10 @@ class FusedAdamW:
             flat = [v for r in rows for e in r for v in (*e, 0.0)]  # mdemi_adamw_group: 5 floats + pad
             t = torch.tensor(flat, dtype=torch.float32)
             self._sched_dev = (t.to(dev), len(rows))
-            self._step_dev = torch.full((1,), taken, dtype=torch.int32, device=dev)
+            if self._step_dev is None:
+                self._step_dev = torch.full((1,), taken, dtype=torch.int32, device=dev)
+            else:  # keep the address a captured graph recorded
+                self._step_dev.fill_(taken)
         return self._sched_dev
 
     def zero_grad(self, set_to_none=True):
@@ -80,8 +101,11 @@ class FusedAdamW:
                 elif p.grad is not None:
                     p.grad.zero_()
 
+    def _with_grad(self):
+        return [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+
     def _refs(self):
-        refs, items_t, items_c = [], [], []
+        refs, items_t, items_c, slots = [], [], [], []
         for gi, g in enumerate(self.param_groups):
             for p in g["params"]:
                 if p.grad is None:
@@ -95,28 +119,41 @@ class FusedAdamW:
                 r = L.TensorRef()
                 r.param, r.grad = p.data_ptr(), p.grad.data_ptr()
                 r.exp_avg, r.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
-                r.numel, r.group = p.numel(), gi
+                r.numel, r.group, r.step_slot = p.numel(), gi, self._slot[p]
                 ti = len(refs)
                 refs.append(r)
+                slots.append(self._slot[p])
                 nch = max(1, math.ceil(p.numel() / self._chunk))
                 items_t.extend([ti] * nch)
                 items_c.extend(range(nch))
-        return refs, items_t, items_c
+        return refs, items_t, items_c, slots
+
+    def _key(self, params):
+        """Every address the pointer table holds: a param, its grad, its state."""
+        key = []
+        for p in params:
+            st = self.state.get(p)
+            key.append((p.data_ptr(), p.grad.data_ptr(),
+                        st["exp_avg"].data_ptr() if st else 0, st["exp_avg_sq"].data_ptr() if st else 0))
+        return tuple(key)
 
     @torch.no_grad()
     def step(self):
-        params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+        params = self._with_grad()
         if not params:
             return
-        self.step_count += 1
+        capturing = torch.cuda.is_current_stream_capturing()
         dev = torch.device("cuda", torch.cuda.current_device())
         lib = L.load()
-        # device table of (param, grad, state) pointers: rebuilt only when a .grad moved
-        # (set_to_none), so a step with persistent gradients (captured graphs, DDP bucket
-        # views) issues no host->device copy at all
-        key = tuple(p.grad.data_ptr() for p in params)
-        if key != getattr(self, "_tbl_key", None):
-            refs, items_t, items_c = self._refs()
+        # device table of (param, grad, state) pointers: rebuilt only when an address moved
+        # (set_to_none grads, replaced param storage, loaded state), so a step with
+        # persistent tensors (captured graphs, DDP bucket views) issues no host->device copy
+        key = self._key(params)
+        if key != self._tbl_key:
+            if capturing:
+                raise RuntimeError("FusedAdamW: the pointer table must be built before hipGraph capture "
+                                   "(run one eager step with the same gradients first)")
+            refs, items_t, items_c, slots = self._refs()
             nt, ni = len(refs), len(items_t)
             raw = (L.TensorRef * nt)(*refs)
             rb = (ctypes.sizeof(raw) + 255) // 256 * 256
@@ -126,25 +163,40 @@ class FusedAdamW:
             host[rb:rb + 8 * ni].view(torch.int32).copy_(torch.tensor(items_t + items_c, dtype=torch.int32))
             dev_buf = host.to(dev, non_blocking=True)
             self._tbl = (host, dev_buf, dev_buf.data_ptr(), dev_buf.data_ptr() + rb, nt, ni)
-            self._tbl_key = key
+            self._tbl_key = self._key(params)
+            self._tbl_slots = slots
+            self.layout_version += 1
         _, _, tl_ptr, ws_ptr, nt, ni = self._tbl
+        if self._steps_dev is None:
+            if capturing:
+                raise RuntimeError("FusedAdamW: step counters must exist before hipGraph capture")
+            self._steps_dev = torch.tensor(self.steps, dtype=torch.int32).to(dev)
         if self._sumsq is None:
             self._sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
         if self.max_grad_norm > 0:
             L.check(lib.mdemi_grad_sumsq(tl_ptr, nt, ni, self._sumsq.data_ptr(), ws_ptr, L.stream()), "grad_sumsq")
         clip = self._sumsq.data_ptr() if self.max_grad_norm > 0 else None
+        steps_ptr = self._steps_dev.data_ptr()
         if self.capturable:
-            sched, nsteps = self._device_schedule(dev, self.step_count - 1)
+            sched, nsteps = self._device_schedule(dev, self.step_count)
             L.check(lib.mdemi_adamw_step_dev(tl_ptr, nt, sched.data_ptr(), nsteps, len(self.param_groups),
-                                             self._step_dev.data_ptr(), clip, self.max_grad_norm, ni, ws_ptr,
-                                             L.stream()), "adamw_step_dev")
+                                             self._step_dev.data_ptr(), steps_ptr, clip, self.max_grad_norm, ni,
+                                             ws_ptr, L.stream()), "adamw_step_dev")
         else:
             groups = (L.AdamWGroup * len(self.param_groups))()
             for i, g in enumerate(self.param_groups):
                 groups[i].lr, (groups[i].beta1, groups[i].beta2) = g["lr"], g["betas"]
                 groups[i].eps, groups[i].weight_decay = g["eps"], g["weight_decay"]
             L.check(lib.mdemi_adamw_step(tl_ptr, nt, groups, len(self.param_groups), clip, self.max_grad_norm,
-                                         self.step_count, ni, ws_ptr, L.stream()), "adamw_step")
+                                         self.step_count + 1, steps_ptr, ni, ws_ptr, L.stream()), "adamw_step")
+        if not capturing:  # a capture records the step; replays advance the mirrors (replayed())
+            self.replayed()
+
+    def replayed(self):
+        """Advance the host mirrors by one executed step over the current table's parameters."""
+        self.step_count += 1
+        for s in self._tbl_slots:
+            self.steps[s] += 1
 
     def state_dict(self):
         """torch.optim.AdamW's layout: state keyed by each parameter's position across
@@ -157,7 +209,7 @@ class FusedAdamW:
             for p in g["params"]:
                 st = self.state.get(p)
                 if st is not None:
-                    state[idx] = {"step": torch.tensor(float(self.step_count)), "exp_avg": st["exp_avg"],
+                    state[idx] = {"step": torch.tensor(float(self.steps[self._slot[p]])), "exp_avg": st["exp_avg"],
                                   "exp_avg_sq": st["exp_avg_sq"]}
                 ids.append(idx)
                 idx += 1
@@ -168,6 +220,13 @@ class FusedAdamW:
         return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd):
+        """Load torch.optim.AdamW's layout (or our own state_dict).  Existing state tensors
+        and step counters are overwritten in place, so a captured train step keeps valid
+        addresses; state for a parameter that had none bumps ``layout_version``."""
+        if "param_groups" not in sd or any("params" not in g for g in sd["param_groups"]):
+            raise ValueError("FusedAdamW.load_state_dict: expected torch.optim.AdamW's layout (per-group 'params' "
+                             "index lists, per-parameter 'step'); optimizer states written by the round-1 "
+                             "FusedAdamW (top-level 'step') are not supported -- re-save them with this version")
         params = [p for g in self.param_groups for p in g["params"]]
         if len(sd["param_groups"]) != len(self.param_groups):
             raise ValueError("loaded state dict has a different number of parameter groups")
@@ -176,18 +235,37 @@ class FusedAdamW:
             raise ValueError("loaded state dict contains a parameter group that doesn't match the size of the "
                              "optimizer's group")
         pos = {int(i): params[k] for k, i in enumerate(order)}
-        self.state = {}
-        steps = [0]
+        new_state, steps, fresh = {}, [0] * len(self.steps), False
         for i, v in sd["state"].items():
             p = pos[int(i)]
-            self.state[p] = {k: v[k].detach().to(p.device, torch.float32).clone() for k in ("exp_avg", "exp_avg_sq")}
-            steps.append(int(float(v.get("step", 0))))
-        self.step_count = max(steps)
+            old = self.state.get(p)
+            ent = {}
+            for k in ("exp_avg", "exp_avg_sq"):
+                src = v[k].detach().to(p.device, torch.float32)
+                if old is not None and old[k].shape == src.shape:
+                    old[k].copy_(src)
+                    ent[k] = old[k]
+                else:
+                    ent[k] = src.clone()
+                    fresh = True
+            new_state[p] = ent
+            steps[self._slot[p]] = int(float(v.get("step", 0)))
+        if fresh or set(new_state) != set(self.state):
+            self.layout_version += 1
+        self.state = new_state
+        self.steps = steps
+        self.step_count = max(steps) if steps else 0
+        if self._steps_dev is not None:
+            self._steps_dev.copy_(torch.tensor(steps, dtype=torch.int32))
+        if self._step_dev is not None:
+            self._step_dev.fill_(self.step_count)
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             g.update({k: v for k, v in sg.items() if k in ("lr", "betas", "eps", "weight_decay", "initial_lr",
                                                           "max_lr", "min_lr", "max_momentum", "base_momentum")})
-        self._tbl_key = None
-        self._sched_dev = None
+        if self._sched_rows is None and self._sched_dev is not None:  # constant-hyperparameter table: refresh
+            rows = [[(g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"]) for g in self.param_groups]]
+            flat = [v for r in rows for e in r for v in (*e, 0.0)]
+            self._sched_dev[0].copy_(torch.tensor(flat, dtype=torch.float32))
 
 
 class OneCycleLR:

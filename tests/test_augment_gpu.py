@@ -98,7 +98,7 @@ def test_dataset_decode_and_gpu_transform(tmp_path):
         Image.fromarray(dd).save(tmp_path / "gts" / f"d{i}.png")
         lines.append(f"i{i}.png d{i}.png 721.5377\n")
     ds = DepthDataset(str(tmp_path), "KITTI", "train", filenames=lines)
-    batch = collate_raw([ds[0], ds[1]])
+    batch = collate_raw([ds[0], ds[1]], pin=True)
     assert batch["image"].shape == (2, 352, 1216, 3) and batch["focal"][0].item() == pytest.approx(721.5377)
     tf = ds.transform()
     img, d, params = tf(batch["image"], batch["depth"], rnd=random.Random(3))

@@ -443,6 +443,47 @@ def test_fused_adamw_with_clip_matches_torch(mf):
         close(a, b, rtol=1e-5, atol=1e-6)
 
 
+def test_fused_adamw_per_parameter_steps_match_torch(mf):
+    """A parameter whose gradient first appears at step 3 is bias-corrected as its own
+    step 1 (torch's per-parameter state["step"]); resuming from torch's state_dict keeps
+    those counts (optim.py FusedAdamW)."""
+    from mdemi.train import FusedAdamW
+    torch.manual_seed(1)
+    shapes = [(64, 3), (9,), (1,)]
+    ps = [torch.randn(*s, device=DEV) for s in shapes]
+    pr = [p.clone().requires_grad_() for p in ps]
+    pg = [p.clone().requires_grad_() for p in ps]
+    ref = torch.optim.AdamW(pr, lr=1e-2, weight_decay=0.05)
+    opt = FusedAdamW(pg, lr=1e-2, weight_decay=0.05)
+    for it in range(5):
+        live = [0, 1] if it < 2 else [0, 1, 2]  # parameter 2 gets gradients from step 3 on
+        for i in range(3):
+            g = torch.randn(*shapes[i], device=DEV) if i in live else None
+            pr[i].grad = None if g is None else g.clone()
+            pg[i].grad = None if g is None else g.clone()
+        ref.step()
+        opt.step()
+    torch.cuda.synchronize()
+    assert opt.steps == [5, 5, 3]
+    for a, b in zip(pg, pr):
+        close(a, b, rtol=1e-5, atol=1e-6)
+    # resume a fresh optimizer from torch's state and take two more steps on both
+    pq = [p.detach().clone().requires_grad_() for p in pg]
+    opt2 = FusedAdamW(pq, lr=1e-2, weight_decay=0.05)
+    opt2.load_state_dict(ref.state_dict())
+    assert opt2.steps == [5, 5, 3]
+    for it in range(2):
+        for i in range(3):
+            g = torch.randn(*shapes[i], device=DEV)
+            pr[i].grad, pq[i].grad = g.clone(), g.clone()
+        ref.step()
+        opt2.step()
+    for a, b in zip(pq, pr):
+        close(a, b, rtol=1e-5, atol=1e-6)
+    sd = opt2.state_dict()
+    assert [int(sd["state"][i]["step"]) for i in range(3)] == [7, 7, 5]
+
+
 def test_headconv(mf):
     n, c, h, w = 2, 128, 9, 11
     x, wt, b = rnd(n, c, h, w, seed=100), rnd(1, c, 3, 3, seed=101, scale=0.1), rnd(1, seed=102)

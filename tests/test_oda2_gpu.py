@@ -1,0 +1,196 @@
+"""ODA2 ordered-swin2 on the GPU against golden vectors produced by the
+reference itself (tests/golden/make_golden_oda2.py): the Swin stage with replicate padding
+(window pad + the merge's swapped pad), the backbone through the patch-embedding quirk,
+the ordered window self-attention (depth-index bias, shift 0 / 4) including the returned
+probabilities, the GLU + replicate depthwise feed-forward, the reducer head and the whole
+wrapper at NYU 480x640 (resized to 448x672 inside) with activation checkpointing on.
+fp32 kernels vs the fp32 reference: outputs within 1e-4, gradients within 1e-3 (relative to
+each tensor's largest magnitude), as the other model tests.
+
+The head's depth indices are floor(sigmoid(logit) * n - 1e-3) (:247-253), discontinuous in
+the logit: where the GPU's and the reference's fp32 logits straddle an integer the index
+legitimately differs.  The tests accept such a flip only within 1e-4 of the boundary, then
+feed the reference's indices on so the rest of the graph is compared like for like."""
+import copy
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import GOLDEN, Golden
+from test_models_gpu import load_golden_weights, nchw_to_nhwc, run_case
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+VANISHING = re.compile(r"(^|\.)(encoder\.norm\d\.bias|k_proj\.bias)$")  # see tests/test_oracle_oda2.py
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from mdemi import _lib
+    return _lib.load()
+
+
+@pytest.mark.parametrize("hw", [(9, 13), (10, 12)])
+def test_oda2_swin_stage_replicate_pad(lib, hw):
+    from mdemi.model.ODA2.oda2_swin_transformer import PatchMerging, SwinTransformerStage
+    H, W = hw
+    g = Golden(f"oda2_swin_stage_{H}x{W}")
+    m = SwinTransformerStage(dim=64, depth=2, num_heads=2, window_size=7, downsample=PatchMerging)
+
+    def fwd(m, i):
+        r = m(i["x"], H, W)
+        return r[0], r[3]
+
+    assert run_case(g, m, fwd, ["x_out", "x_down"], {}, {}) > 10
+
+
+def test_oda2_swin_backbone_patch_embed_quirk(lib):
+    from mdemi.model.ODA2.oda2_swin_transformer import SwinTransformer
+    g = Golden("oda2_swin_backbone")
+    m = SwinTransformer(embed_dim=32, depths=(2, 2, 2, 2), num_heads=(1, 2, 4, 8), window_size=7, path_drop_prob=0.0)
+    run_case(g, m, lambda m, i: m(i["img"]), ["o0", "o1", "o2", "o3"], {f"o{k}": "nchw" for k in range(4)},
+             {}, no_input_grad=("img",))
+
+
+@pytest.mark.parametrize("shift", [0, 4])
+def test_oda2_ordered_window_attention(lib, shift):
+    from mdemi.model.ODA2 import PreNormOrderedSwinSA
+    g = Golden(f"oda2_ordered_sa_shift{shift}")
+    m = PreNormOrderedSwinSA(64, 4, num_emb=16, window_size=8, shift_size=shift)
+    idx = torch.from_numpy(np.random.Generator(np.random.PCG64(63)).integers(0, 16, (2, 16, 24))).to(DEV)
+    run_case(g, m, lambda m, i: m(i["x"], idx), ["y", "attn"], {}, {}, vanishing=VANISHING)
+
+
+def test_oda2_dwconv_ff(lib):
+    from mdemi.model.ODA2 import PreNormDWConvFF
+    g = Golden("oda2_dwconv_ff")
+    run_case(g, PreNormDWConvFF(32, feedforward_dims=64), lambda m, i: m(i["x"]), ["y"], {}, {})
+
+
+def _pin_indices(head, golden_idx, seen):
+    """Replace head._logit_to_indices: compute the GPU's own indices, check them against the
+    reference's (flips only on a floor boundary), return the reference's."""
+    orig = head._logit_to_indices
+    n = head.num_emb
+
+    def pinned(logit):
+        ours = orig(logit)
+        k = len(seen)
+        want = torch.from_numpy(golden_idx[k].astype(np.int64)).to(ours.device).to(ours.dtype)
+        diff = ours != want
+        if diff.any():
+            v = torch.sigmoid(logit.detach().double()).squeeze(-1) * n - 1e-3
+            dist = (v - torch.round(v)).abs()
+            assert (dist[diff] < 1e-4).all(), f"index mismatch away from a floor boundary (repeat {k})"
+        seen.append(int(diff.sum()))
+        return want
+
+    head._logit_to_indices = pinned
+
+
+def test_oda2_reg_head(lib):
+    from mdemi.model.ODA2 import OrderedSwinRegHead
+    g = Golden("oda2_reg_head")
+    m = OrderedSwinRegHead(64, 4, 2, num_emb=16, window_size=8)
+    gidx = [g.d[f"idx/{k}"] for k in range(len(g.keys("idx/")))]
+    seen = []
+    _pin_indices(m, gidx, seen)
+
+    def fwd(m, i):
+        outs, attn = m(i["x"])
+        return tuple(outs) + tuple(attn)
+
+    run_case(g, m, fwd, ["out0", "out1", "out2"] + [f"attn{k}" for k in range(4)], {}, {}, vanishing=VANISHING)
+    assert len(seen) == 2 and sum(seen) <= 3
+
+
+def _small_model(neck, use_checkpoint):
+    from mdemi.model.ODA2 import ODA2OrderedSwin2RegModel
+    with open(os.path.join(GOLDEN, "meta.json")) as f:
+        meta = json.load(f)[f"oda2_model_{neck}"]
+    e = meta["encoder"]
+    return ODA2OrderedSwin2RegModel(dec_dim=meta["dec_dim"], min_depth=1e-3, max_depth=meta["max_depth"],
+                                    num_heads=meta["num_heads"], num_repeats=meta["num_repeats"],
+                                    num_emb=meta["num_emb"], window_size=meta["window_size"], neck_type=neck,
+                                    use_checkpoint=use_checkpoint, path_drop_prob=0.0,
+                                    encoder_kwargs=dict(embed_dim=e["embed_dim"], depths=tuple(e["depths"]),
+                                                        num_heads=tuple(e["num_heads"])))
+
+
+@pytest.mark.parametrize("neck", ["red", "red33"])
+def test_oda2_model_end_to_end(lib, neck):
+    """The wrapper at NYU 480x640 (use_checkpoint=True, as the reference builds it): depth,
+    the intermediate outputs and every parameter gradient (sums) against the reference."""
+    g = Golden(f"oda2_model_{neck}")
+    m = _small_model(neck, use_checkpoint=True)
+    gidx = [g.d[f"idx/{k}"] for k in range(len(g.keys("idx/")))]
+    seen = []
+    _pin_indices(m.decoder.reducer, gidx, seen)
+
+    def fwd(m, i):
+        out, outs, attn = m(i["img"])
+        assert len(attn) == 2 * m.num_repeats and out is outs[-1]
+        return (out,) + tuple(outs[:-1])
+
+    n = run_case(g, m, fwd, ["depth", "out0", "out1"], {}, {}, no_input_grad=("img",), vanishing=VANISHING)
+    assert n == sum(1 for k in g.d.keys() if k.startswith("gsum/"))
+
+
+def test_oda2_checkpointing_is_numerically_transparent(lib):
+    """Activation checkpointing (oda2_swin_transformer.py:442-443) recomputes each Swin block
+    in the backward; outputs and gradients equal the stored-activation run's (the
+    recomputation replays the same kernels on the same inputs)."""
+    torch.manual_seed(0)
+    ma = _small_model("red", use_checkpoint=True).to(DEV).train()
+    mb = _small_model("red", use_checkpoint=False).to(DEV).train()
+    mb.load_state_dict(ma.state_dict())
+    img = torch.randn(2, 3, 480, 640, device=DEV)
+    res = []
+    for m in (ma, mb):
+        out, outs, _ = m(img)
+        (out.square().mean() + outs[0].mean()).backward()
+        res.append((out.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    assert torch.equal(res[0][0], res[1][0])
+    for k in res[0][1]:
+        a, b = res[0][1][k], res[1][1][k]
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * (b.abs().max().item() + 1e-30)), k
+
+
+def test_oda2_large_kitti_train_step(lib):
+    """Full size: Swin-L + dec_dim 512, 3 repeats (json/kitti/oda2/oda2_red_order_swin2.json)
+    at KITTI 352x704 (resized to 448x896), batch 2: one train step through the config-driven
+    trainer (SILog on every output, clipped AdamW) -- shapes, finiteness, every parameter
+    moved; and the model's own forward at the 352x1216 test shape (448x1536: the stage-1
+    windows pad by replication)."""
+    from mdemi.train import build_from_config
+    opt = {"model": {"name": "oda2_red_order_swin2", "encoder_type": "large", "dec_dim": 512, "num_heads": 8,
+                     "num_repeats": 3, "num_emb": 128, "window_size": 8, "drop_prob": 0.0, "attn_drop_prob": 0.0,
+                     "bn_momentum": 0.1},
+           "loss": {"alpha": 10.0, "beta": 0.15, "per_image": True, "si_weight": 1.0},
+           "dataset": {"data_type": "KITTI"}, "dataloader": {"batch_size": 2},
+           "optimizer": {"lr": 1e-4, "weight_decay": 0.1, "eps": 1e-6, "same_lr": True},
+           "scheduler": {"name": "onecycle", "pct_start": 0.25, "div_factor": 25, "final_div_factor": 100,
+                         "cycle_momentum": False},
+           "train": {"epoch": 1, "num_accum": 1, "grad_norm": 0.1},
+           "eval": {"max_depth_eval": 80, "min_depth_eval": 0.001}}
+    torch.manual_seed(0)
+    tr = build_from_config(copy.deepcopy(opt), device=DEV, steps_per_epoch=10)
+    g = torch.Generator().manual_seed(5)
+    img = torch.randn(2, 3, 352, 704, generator=g).to(DEV)
+    gt = (torch.rand(2, 1, 352, 704, generator=g) * 79 + 1).to(DEV)
+    before = {k: p.detach().clone() for k, p in tr.model.named_parameters()}
+    loss = tr.step([(img, gt)])
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item()
+    moved = sum(int(not torch.equal(before[k], p.detach())) for k, p in tr.model.named_parameters())
+    assert moved == len(before), (moved, len(before))
+    tr.model.eval()
+    with torch.no_grad():
+        out, outs, attn = tr.model(torch.randn(1, 3, 352, 1216, device=DEV))
+    assert out.shape == (1, 1, 112, 384) and len(outs) == 4 and len(attn) == 6
+    assert torch.isfinite(out).all() and (out > 0).all() and (out < 80).all()
+    assert attn[0].shape == (1 * 14 * 48, 8, 64, 64)

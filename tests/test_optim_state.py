@@ -31,12 +31,14 @@ def test_torch_adamw_state_loads_into_fused():
     ours = FusedAdamW([{"params": qs[:2], "lr": 1e-3}, {"params": qs[2:], "lr": 1e-4}], weight_decay=0.1)
     ours.load_state_dict(sd)
     assert ours.step_count == 2
+    assert ours.steps == [1, 2, 2]  # ps[0] first had a gradient at step 2: its own count is 1
     for p, q in zip(ps, qs):
         for k in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(ours.state[q][k], ref.state[p][k])
     # and back into torch
     sd2 = ours.state_dict()
     assert sorted(sd2["state"]) == [0, 1, 2] and [g["params"] for g in sd2["param_groups"]] == [[0, 1], [2]]
+    assert [float(sd2["state"][i]["step"]) for i in range(3)] == [float(ref.state[p]["step"]) for p in ps]
     ref2 = torch.optim.AdamW([{"params": ps[:2], "lr": 1e-3}, {"params": ps[2:], "lr": 1e-4}], weight_decay=0.1)
     ref2.load_state_dict(sd2)
     for p in ps:
@@ -52,6 +54,7 @@ def test_state_keyed_by_position_not_first_gradient():
     for i in (2, 0):
         opt.state[ps[i]] = {"exp_avg": torch.full_like(ps[i], float(i + 1)), "exp_avg_sq": torch.zeros_like(ps[i])}
     opt.step_count = 3
+    opt.steps = [3, 0, 2]
     sd = opt.state_dict()
     assert sorted(sd["state"]) == [0, 2]
     assert torch.equal(sd["state"][2]["exp_avg"], torch.full((5,), 3.0))
@@ -61,3 +64,15 @@ def test_state_keyed_by_position_not_first_gradient():
     assert qs[1] not in opt2.state
     assert torch.equal(opt2.state[qs[2]]["exp_avg"], torch.full((5,), 3.0))
     assert torch.equal(opt2.state[qs[0]]["exp_avg"], torch.full((3, 2), 1.0))
+    assert opt2.steps == [3, 0, 2]
+
+
+def test_round1_layout_is_rejected_with_a_clear_error():
+    import pytest
+    from mdemi.train import FusedAdamW
+    ps = _params()
+    opt = FusedAdamW(ps, lr=1e-3)
+    old = {"step": 4, "state": {0: {"exp_avg": torch.zeros(5), "exp_avg_sq": torch.zeros(5)}},
+           "param_groups": [{"lr": 1e-3}]}
+    with pytest.raises(ValueError, match="round-1"):
+        opt.load_state_dict(old)
