@@ -74,6 +74,18 @@ _DFV8_NYU = {  # json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.
     "train": {"epoch": 50, "num_accum": 1, "grad_norm": 0.1},
     "eval": {"max_depth_eval": 10, "min_depth_eval": 0.001, "garg_crop": False, "eigen_crop": True}}
 
+_ODA2_KITTI = {  # json/kitti/oda2/oda2_red_order_swin2.json
+    "model": {"name": "oda2_red_order_swin2", "encoder_type": "large", "dec_dim": 512, "num_heads": 8,
+              "num_repeats": 3, "num_emb": 128, "window_size": 8, "drop_prob": 0.0, "attn_drop_prob": 0.0,
+              "bn_momentum": 0.1},
+    "loss": {"alpha": 10.0, "beta": 0.15, "per_image": True, "si_weight": 1.0},
+    "dataset": {"data_type": "KITTI"}, "dataloader": {"batch_size": 8},
+    "optimizer": {"lr": 1e-4, "betas": [0.9, 0.999], "weight_decay": 0.1, "eps": 1e-6, "same_lr": True},
+    "scheduler": {"name": "onecycle", "pct_start": 0.25, "div_factor": 25, "final_div_factor": 100,
+                  "cycle_momentum": False},
+    "train": {"epoch": 24, "num_accum": 2, "grad_norm": 0.1},
+    "eval": {"max_depth_eval": 80, "min_depth_eval": 0.001, "garg_crop": True, "eigen_crop": False}}
+
 WORKLOADS = {
     "newcrfs": dict(opt=_NEWCRFS_NYU, model="NewCRFs-L07", h=480, w=640,
                     workload="NewCRFs Swin-L (large07) train step, NYU 480x640",
@@ -92,7 +104,16 @@ WORKLOADS = {
     "depthformer_bf16": dict(opt=_DFV8_NYU, model="DepthformerV8-B5", h=480, w=640, precision="bf16", graph=True,
                              workload="Depthformer v8 train step, NYU 480x640, bf16 mixed precision, hipGraph",
                              ref_cfg="json/kitti/depthformer/depthformer_v8_cham_loss_per_image_4gpu.json"),
+    # SURVEY §8f-4 (not a BASELINE config): ODA2 ordered-swin2, KITTI 352x704 (resized to 448x896
+    # inside), batch 8 x num_accum 2 as configured
+    "oda2": dict(opt=_ODA2_KITTI, model="ODA2-OrderedSwin2-L", h=352, w=704,
+                 workload="ODA2 ordered-swin2 (Swin-L) train step, KITTI 352x704",
+                 ref_cfg="json/kitti/oda2/oda2_red_order_swin2.json"),
 }
+# The default line (BASELINE.json metric, NeW-CRFs NYU) carries every other single-GPU
+# BASELINE config as a compact secondary: configs[2] (NeW-CRFs KITTI 352x1216 bs 8),
+# configs[1] (AdaBins NYU bs 16) and configs[4] at N GPUs (Depthformer v8 bf16 + hipGraph).
+SECONDARIES = {"newcrfs_kitti": 8, "adabins": 16, "depthformer_bf16": 8}
 # HBM bytes per launch of the roofline kernel family, from the committed
 # rocprofv3 --pmc passes (tools/pmc_traffic.py; FETCH_SIZE doubled per the
 # gfx950 correction).  None when no profile matches the kernel.
@@ -113,7 +134,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the KITTI 352x1216 secondary line")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the secondary workloads")
+    ap.add_argument("--secondaries", default=",".join(SECONDARIES),
+                    help="comma list of secondary workloads on the default line (subset of " +
+                         ",".join(SECONDARIES) + ")")
     ap.add_argument("--precision", default=None, choices=["fp32", "fp32e", "bf16"],
                     help="matmul precision (default: the workload's). fp32: exact-product fp32 MFMA; fp32e: "
                          "fp32 via three exact bf16 planes on the bf16 MFMA (fp32 error); bf16: bf16 operands, "
@@ -146,6 +170,11 @@ def launch_ranks(args):
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
     return subprocess.call(cmd, env=env)
+
+
+def _progress(msg):
+    """A line on stderr per bench phase (the GPU harness kills a command silent for 3 min)."""
+    print(f"bench[{os.environ.get('RANK', '0')}]: {msg}", file=sys.stderr, flush=True)
 
 
 # --------------------------------------------------------------------------- data
@@ -352,6 +381,21 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
+def _usable_cpus():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(model, opt, H, W, budget_s):
     """The oracle (CPU restatement of the reference path: oracle/newcrfs.py, oracle/adabins.py,
     oracle/depthformer.py) timed on the host cores: fp32 forward + loss + backward + clipped
@@ -394,19 +438,34 @@ def cpu_baseline(model, opt, H, W, budget_s):
         copt.step()
         copt.zero_grad(set_to_none=True)
 
-    t0 = time.perf_counter()
-    step()
-    step()  # 2 warm-up steps
-    per = (time.perf_counter() - t0) / 2
-    n = max(1, min(5, int(budget_s / max(per, 1e-3))))
-    t0 = time.perf_counter()
-    for _ in range(n):
+    def timed(threads, budget):
+        torch.set_num_threads(threads)
+        t0 = time.perf_counter()
         step()
-    dt = (time.perf_counter() - t0) / n
-    return {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle {name} fp32 train step (fwd+SILog{'+chamfer' if cham else ''}+bwd+clip+AdamW), "
-                      f"batch 1 at {H}x{W}, {n} timed steps after 2 warm-up, {threads} threads (the box's "
-                      f"per-GPU CPU share), {os.cpu_count()} host CPUs visible, CPU: {_cpu_model()}"}
+        step()  # 2 warm-up steps
+        per = (time.perf_counter() - t0) / 2
+        n = max(1, min(5, int(budget / max(per, 1e-3))))
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+        return (time.perf_counter() - t0) / n, n
+
+    dt, n = timed(threads, budget_s)
+    res = {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+           "sample": f"oracle {name} fp32 train step (fwd+SILog{'+chamfer' if cham else ''}+bwd+clip+AdamW), "
+                     f"batch 1 at {H}x{W}, {n} timed steps after 2 warm-up, {threads} threads (the box's "
+                     f"per-GPU CPU share), {os.cpu_count()} host CPUs visible, CPU: {_cpu_model()}"}
+    # SURVEY §8d asks for every physical core: the same sample on all the CPUs this process may
+    # actually use (affinity, capped by the cgroup CPU quota -- oversubscribing a quota only
+    # slows the sample down), reported beside the share when that is more
+    allc = _usable_cpus()
+    _progress(f"cpu_baseline: {threads} threads {1.0 / dt:.3f} img/s; usable CPUs {allc}")
+    res["usable_cpus"] = allc
+    if allc > threads and budget_s > 0:
+        dt2, n2 = timed(allc, budget_s / 2)
+        res["all_cores"] = {"value": round(1.0 / dt2, 4), "cores": allc, "timed_steps": n2}
+    torch.set_num_threads(threads)
+    return res
 
 
 # --------------------------------------------------------------------------- one measurement
@@ -420,9 +479,11 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
     na = trainer.num_accum
     batches = [synthetic_batch(B, H, W, device, seed=1000 + 7 * rank + i, data_type=opt["dataset"]["data_type"])
                for i in range(na)]
+    _progress(f"{key}: built (B={B} {H}x{W} {precision}{' graph' if graph else ''}), warm-up")
     for _ in range(args.warmup):
         trainer.step(batches)
     torch.cuda.synchronize()
+    _progress(f"{key}: timing {args.steps} steps")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -452,11 +513,44 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
         res["allreduce"] = {"grad_bytes": sum(ddp.bucket_bytes), "buckets": len(ddp.buckets),
                             "isolated_ms": round(iso, 2), "share_of_step_upper_bound": round(iso / res["ms"], 4),
                             "bus_GBps": round(2 * (world - 1) / world * sum(ddp.bucket_bytes) / (iso * 1e-3) / 1e9, 1)}
+    _progress(f"{key}: {res['ms']:.1f} ms/step")
     if with_roofline:
         res["roofline"], res["extra"] = roofline_entry(trainer, batches, key, res["ms"])
         if getattr(trainer, "_hbm_kernels", None):
             res["extra"]["hbm_kernels"] = trainer._hbm_kernels
     return res
+
+
+def measure_secondary(args, sk, rank, world, device):
+    """One secondary BASELINE workload: fewer timed steps than the headline (each is a
+    whole-model train step, so 5 steps already average over every kernel), its own
+    instrumented roofline step and HBM-kernel rates."""
+    wk = WORKLOADS[sk]
+    B = SECONDARIES[sk]
+    prec = wk.get("precision", "fp32")
+    graph = wk.get("graph", False)
+    sub = argparse.Namespace(**vars(args))
+    sub.steps = max(3, min(args.steps, 5))
+    sub.warmup = max(3 if graph else 1, min(args.warmup, 3))  # a captured step: 2 eager + the capture
+    sec = measure(sub, wk["opt"], sk, wk["h"], wk["w"], B, rank, world, device, with_roofline=not args.no_roofline,
+                  precision=prec, graph=graph)
+    del sec["trainer"]
+    out = {"workload": wk["workload"], "reference_config": wk["ref_cfg"], "per_gpu_batch": B,
+           "image": [wk["h"], wk["w"]], "matmul_precision": prec, "hipgraph": graph, "steps": sub.steps,
+           "images_per_sec": round(sec["images"] / sec["elapsed"], 3), "ms_per_step": round(sec["ms"], 2),
+           "loss": round(sec["loss"], 5)}
+    if "roofline" in sec:
+        out["roofline"] = sec["roofline"]
+        out["step_mfma_frac"] = sec["extra"]["step_mfma_frac"]
+        out["gemm_all_frac"] = sec["extra"]["gemm_all"]["frac"]
+        if "hbm_kernels" in sec["extra"]:
+            out["hbm_kernels"] = sec["extra"]["hbm_kernels"]
+        if sk == "newcrfs_kitti":  # SURVEY §8d: 2404.7 GFLOP per image per train step at 352x1216
+            out["survey_flop_frac"] = round(2404.7e9 * sec["images"] / sec["elapsed"] / world / 1e12 /
+                                            FP32_MFMA_PEAK_TFLOPS, 4)
+    if "allreduce" in sec:
+        out["allreduce"] = sec["allreduce"]
+    return out
 
 
 # --------------------------------------------------------------------------- plumbing (CPU)
@@ -570,21 +664,12 @@ def main():
 
     secondary = None
     if key == "newcrfs" and not args.no_secondary and args.batch is None and args.height is None:
-        wk = WORKLOADS["newcrfs_kitti"]
-        sec = measure(args, wk["opt"], "newcrfs_kitti", wk["h"], wk["w"], 8, rank, world, device,
-                      with_roofline=not args.no_roofline, precision=precision)
-        del sec["trainer"]
-        secondary = {"workload": wk["workload"], "reference_config": wk["ref_cfg"], "per_gpu_batch": 8,
-                     "images_per_sec": round(sec["images"] / sec["elapsed"], 3), "ms_per_step": round(sec["ms"], 2),
-                     "loss": round(sec["loss"], 5)}
-        if "roofline" in sec:
-            secondary["roofline"] = sec["roofline"]
-            secondary["step_mfma_frac"] = sec["extra"]["step_mfma_frac"]
-            # 2404.7 GFLOP per image per train step at 352x1216 (reference flop count)
-            secondary["survey_flop_frac"] = round(2404.7e9 * sec["images"] / sec["elapsed"] / world / 1e12 /
-                                                  FP32_MFMA_PEAK_TFLOPS, 4)
-        if "allreduce" in sec:
-            secondary["allreduce"] = sec["allreduce"]
+        secondary = {}
+        for sk in [k for k in args.secondaries.split(",") if k]:
+            if sk not in SECONDARIES:
+                raise SystemExit(f"bench: unknown secondary {sk!r}")
+            secondary[sk] = measure_secondary(args, sk, rank, world, device)
+            torch.cuda.empty_cache()
 
     if rank == 0:
         line = {
@@ -604,8 +689,10 @@ def main():
         if "allreduce" in res:
             line["allreduce"] = res["allreduce"]
         line.update(res.get("extra", {}))
-        if secondary is not None:
-            line["secondary"] = secondary
+        if secondary:
+            line["secondary"] = secondary.pop("newcrfs_kitti", None)
+            if secondary:
+                line["secondaries"] = secondary
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -253,7 +253,8 @@ class PatchEmbed(nn.Module):
             if pad_b:
                 raise RuntimeError(f"PatchEmbed: the reference's pad adds {pad_b} channels to a {h}x{w} image "
                                    "(F.pad 6-tuple on NCHW, oda2_swin_transformer.py:491) and its conv rejects it")
-            x = mf.replicate_rows_nchw_no_grad(x, h + pad_r, w - w % pw)  # rows replicated, width floored
+            # rows replicated; the stride-p conv floors both sides
+            x = mf.replicate_rows_nchw_no_grad(x, (h + pad_r) - (h + pad_r) % ph, w - w % pw)
         y = mf.patch_embed(x, self.proj.weight, self.proj.bias)
         if self.norm is not None:
             y = mf.layer_norm(y, self.norm.weight, self.norm.bias, self.norm.eps)

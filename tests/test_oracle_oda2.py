@@ -18,8 +18,10 @@ RT_OUT, RT_GRAD = 2e-5, 2e-4
 #  * encoder.norm<i>.bias: every encoder output feeds a (replicate-padded) conv followed by a
 #    train-mode BatchNorm (oda2_red_order_swin2_decoder.py:316-343, ConvBN
 #    oda2_layer_utils.py:47-50), which removes any per-channel constant;
-#  * *.k_proj.bias: adds one constant to every score of a query row, which softmax ignores.
-VANISHING = re.compile(r"(^|\.)(encoder\.norm\d\.bias|k_proj\.bias)$")
+#  * *.k_proj.bias: adds one constant to every score of a query row, which softmax ignores;
+#  * the last ordered block's output-norm bias (reducer.attn_layers.<last>.norm.bias): it
+#    reaches the loss only through the last conv head, again a conv + train-mode BatchNorm.
+VANISHING = re.compile(r"(^|\.)(encoder\.norm\d\.bias|k_proj\.bias|reducer\.attn_layers\.1\.norm\.bias)$")
 
 
 def _run(g, fwd, out_names, rt_grad=RT_GRAD):
