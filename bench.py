@@ -419,17 +419,34 @@ def cpu_baseline(model, opt, H, W, budget_s):
         from oracle import depthformer as odf
         opt_m = dict(opt["model"], attn_drop_prob=0.0, drop_prob=0.0)
         fwd = lambda: odf.depthformer_v8_full(P, img, opt_m, dmin, dmax)  # noqa: E731
+    elif name == "oda2_red_order_swin2":
+        from oracle import oda2 as oo
+        m = opt["model"]
+        enc = {"depths": (2, 2, 18, 2), "num_heads": (6, 12, 24, 48) if m["encoder_type"] in ("large", "L")
+               else (4, 8, 16, 32)}
+        dec = {k: m[k] for k in ("num_heads", "num_repeats", "num_emb")}
+        dec.update(window_size=m.get("window_size", 8), neck_type=m.get("neck_type", "red"),
+                   output_scale=m.get("output_scale", 4), bias_type=m.get("bias_type", "depth"))
+        fwd = lambda: oo.oda2_model(P, img, enc, dec, dmax)[:2]  # noqa: E731  (out, outs)
     else:
         from oracle import newcrfs as onc
         fwd = lambda: onc.newcrf_depth(P, img, "large07", max_depth=dmax)  # noqa: E731
     cham = float(lo.get("chamfer_weight", 0.0))
 
+    def up(p):
+        if p.shape[-2:] != gt.shape[-2:]:
+            p = torch.nn.functional.interpolate(p, gt.shape[-2:], mode="bilinear", align_corners=True)
+        return p
+
     def step():
         out = fwd()
-        pred = out[0] if isinstance(out, tuple) else out
-        if pred.shape[-2:] != gt.shape[-2:]:
-            pred = torch.nn.functional.interpolate(pred, gt.shape[-2:], mode="bilinear", align_corners=True)
-        loss = omet.silog_loss(pred, gt, dmin, lo["alpha"], lo["beta"], lo["per_image"])
+        if name == "oda2_red_order_swin2":  # SILog over every output (train/builder.py TrainLoss)
+            outs = out[1]
+            loss = sum(omet.silog_loss(up(o), gt, dmin, lo["alpha"], lo["beta"], lo["per_image"]) for o in outs)
+            loss = loss * (float(lo.get("si_weight", 1.0)) / len(outs))
+        else:
+            pred = up(out[0] if isinstance(out, tuple) else out)
+            loss = omet.silog_loss(pred, gt, dmin, lo["alpha"], lo["beta"], lo["per_image"])
         if cham > 0:
             from oracle.adabins import bins_chamfer_loss
             loss = loss + cham * bins_chamfer_loss(out[1], gt, dmin, from_edges=(name == "adabins"))
