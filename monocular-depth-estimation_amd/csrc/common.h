@@ -126,6 +126,9 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 size_t colsum_ws_bytes(int64_t rows, int64_t cols);
 int colsum_launch(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, int accumulate, void* ws,
                   hipStream_t st);
+// as colsum_launch, columns >= split_col going to out2[c - split_col]
+int colsum_launch_split(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, float* out2,
+                        int64_t split_col, int accumulate, void* ws, hipStream_t st);
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace mdemi

@@ -83,11 +83,21 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   const int aimg = (wm * WTM) >> 7;
   const int rb0 = wn * 64 + l31, rb1 = rb0 + 32;
 
+#ifdef MDEMI_STUDY_NOLOAD  // study build: no global operand loads (LDS + MFMA + barrier ceiling)
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) ra[a][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) rb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load = [&](int) {};
+#else
   auto load = [&](int kt) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) la[a].load(kt * BK, ra[a]);
     lb.load(kt * BK, rb);
   };
+#endif
   auto stage = [&](float* dst) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) LA::store(dst + a * FA, t, ra[a]);
@@ -128,6 +138,10 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
       MDEMI_STEP(x) MDEMI_STEP(y) MDEMI_STEP(z) MDEMI_STEP(w)
 #undef MDEMI_STEP
     }
+#ifdef MDEMI_STUDY_NOSYNC  // study build: no restaging and no barrier (LDS reads + MFMA ceiling)
+    if (true) {
+    } else
+#endif
     if (!PREF) {
       __syncthreads();
     } else {

@@ -223,6 +223,8 @@ static int ln_bwd_launch(const float* dy, const float* x, const float* mean, con
   if (dgamma || dbeta) {
     float* sums = (float*)((char*)workspace + ln_part_bytes(rows, C));
     void* cws = (char*)sums + align_up((size_t)2 * C * 4, 256);
+    if (dgamma && dbeta)  // the partial sums land in dgamma / dbeta directly
+      return colsum_launch_split(partial, nb, 2 * C, 2 * C, dgamma, dbeta, C, 0, cws, st);
     int rc = colsum_launch(partial, nb, 2 * C, 2 * C, sums, 0, cws, st);
     if (rc) return rc;
     hipLaunchKernelGGL(ln_param_split, dim3((C + 255) / 256), dim3(256), 0, st, sums, dgamma, dbeta, C);

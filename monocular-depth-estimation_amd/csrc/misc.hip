@@ -54,12 +54,48 @@ __global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ 
 }
 
 __global__ void colsum_final(const float* __restrict__ part, int nblk, int64_t cols, float* __restrict__ out,
-                             int accumulate) {
+                             float* __restrict__ out2, int64_t split_col, int accumulate) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cols) return;
   float s = 0.f;
   for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * cols + c];
-  out[c] = accumulate ? out[c] + s : s;
+  float* o = c < split_col ? out + c : out2 + (c - split_col);
+  *o = accumulate ? *o + s : s;
+}
+
+// Short reductions (rows <= COLSUM_ONEPASS): one launch, no workspace.  A block
+// covers 32 columns with 32 row groups; each thread keeps 8 loads in flight
+// (rows ty, ty+32, ... in order), then the 32 group sums are added in group
+// order -- a fixed association, so the result is deterministic.
+constexpr int COLSUM_ONEPASS = 1024;
+__global__ __launch_bounds__(1024) void colsum_onepass(const float* __restrict__ x, int64_t rows, int64_t cols,
+                                                       int64_t ld, float* __restrict__ out, float* __restrict__ out2,
+                                                       int64_t split_col, int accumulate) {
+  __shared__ float red[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t c = (int64_t)blockIdx.x * 32 + tx;
+  float s = 0.f;
+  if (c < cols) {
+    for (int64_t r0 = ty; r0 < rows; r0 += 256) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t r = r0 + 32 * j;
+        v[j] = r < rows ? x[r * ld + c] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) t += red[k][tx];
+    float* o = c < split_col ? out + c : out2 + (c - split_col);
+    *o = accumulate ? *o + t : t;
+  }
 }
 
 static int colsum_blocks_y(int64_t rows) {
@@ -222,17 +258,26 @@ extern "C" int mdemi_elementwise(int32_t op, const float* a, const float* b, flo
 
 namespace mdemi {
 size_t colsum_ws_bytes(int64_t rows, int64_t cols) {
-  return align_up((size_t)colsum_blocks_y(rows) * cols * sizeof(float), 256);
+  return rows <= COLSUM_ONEPASS ? 0 : align_up((size_t)colsum_blocks_y(rows) * cols * sizeof(float), 256);
 }
-int colsum_launch(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, int accumulate, void* ws,
-                  hipStream_t st) {
+int colsum_launch_split(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, float* out2,
+                        int64_t split_col, int accumulate, void* ws, hipStream_t st) {
+  if (rows <= COLSUM_ONEPASS) {
+    hipLaunchKernelGGL(colsum_onepass, dim3((unsigned)cdiv(cols, 32)), dim3(1024), 0, st, x, rows, cols, ld, out,
+                       out2, split_col, accumulate);
+    return check_launch("colsum");
+  }
   const int ny = colsum_blocks_y(rows);
   const int64_t rpb = cdiv(rows, ny);
   dim3 grid((unsigned)cdiv(cols, 32), (unsigned)ny);
   hipLaunchKernelGGL(colsum_partial, grid, dim3(256), 0, st, x, rows, cols, ld, (float*)ws, rpb);
   hipLaunchKernelGGL(colsum_final, dim3((unsigned)cdiv(cols, 256)), dim3(256), 0, st, (const float*)ws, ny, cols, out,
-                     accumulate);
+                     out2, split_col, accumulate);
   return check_launch("colsum");
+}
+int colsum_launch(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, int accumulate, void* ws,
+                  hipStream_t st) {
+  return colsum_launch_split(x, rows, cols, ld, out, nullptr, cols, accumulate, ws, st);
 }
 }  // namespace mdemi
 
@@ -241,7 +286,7 @@ extern "C" size_t mdemi_colsum_workspace_size(int64_t rows, int64_t cols) { retu
 extern "C" int mdemi_colsum_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out, int accumulate,
                                 void* workspace, void* stream) {
   MDEMI_REQUIRE(x && out && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
-  if (!workspace) { set_error("colsum: workspace required"); return MDEMI_EWORKSPACE; }
+  if (!workspace && colsum_ws_bytes(rows, cols) > 0) { set_error("colsum: workspace required"); return MDEMI_EWORKSPACE; }
   return colsum_launch(x, rows, cols, ld, out, accumulate, workspace, (hipStream_t)stream);
 }
 

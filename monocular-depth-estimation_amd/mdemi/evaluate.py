@@ -84,7 +84,7 @@ class GraphedPredictor:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.static_out = predict_depth(model, self.static_in, self.flip_eval)
 
     def __call__(self, img):

@@ -236,7 +236,10 @@ class Trainer:
             if self.ddp is not None:
                 torch.cuda.synchronize()  # no collective of the eager steps may still be in flight
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g), mf.matmul_precision(self.precision):
+            # thread_local: only this thread's capture-unsafe calls are refused -- the RCCL
+            # process group's watchdog thread keeps polling the events of the eager steps'
+            # collectives while we capture (global mode fails its hipEventQuery)
+            with torch.cuda.graph(g, capture_error_mode="thread_local"), mf.matmul_precision(self.precision):
                 self._static_loss = self._body(self._static)
                 self._zero_grad(set_to_none=False)  # gradients keep their (captured) addresses
             self._graph = g
