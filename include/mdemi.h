@@ -116,6 +116,12 @@ typedef struct mdemi_gemm_desc {
                                       buffers).  0/1: one-level batch.  Needs batch %
                                       batch_inner == 0 and no aux/residual/preact/rowsum_a */
   int64_t a_bstride_inner, b_bstride_inner, c_bstride_inner;
+  const float* row_scale; int64_t row_scale_group;  /* optional: the value after `act`
+                                      is multiplied by row_scale[i / row_scale_group]
+                                      before the residual add -- timm DropPath's per-sample
+                                      keep/(1-p) scale of a residual branch
+                                      (swin_transformer.py:232,239) fused into the proj /
+                                      fc2 epilogue.  Batch 1. */
 } mdemi_gemm_desc;
 
 size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d);
@@ -147,6 +153,12 @@ int mdemi_gemm_set_variant(int32_t variant, int32_t group_m);
  * tile with two LDS buffers, 1 = one buffer, 2 = 256-row tile; -1 = per-shape
  * autotune (default; all bit-identical). */
 int mdemi_gemm_set_variant_m16(int32_t variant);
+/* scheduling switches (process-global; defaults on, or from MDEMI_GEMM_TAIL_SPLIT /
+ * MDEMI_GEMM_INLINE_REDUCE = 0): tail_split -- a whole-K GEMM whose tiles leave a thin
+ * last round of workgroups splits the rows of the leftover tiles over K (a plan that
+ * depends on the shape only); inline_reduce -- split-K slabs are combined by the
+ * last-arriving piece of each tile instead of a separate reduce launch. */
+int mdemi_gemm_set_options(int32_t tail_split, int32_t inline_reduce);
 
 /* column / row sums (bias gradients: db[j] = sum_i dY[i][j])
  * replaces the bias-grad reduction autograd runs for every nn.Linear/Conv2d. */

@@ -42,6 +42,12 @@ struct GemmParams {
   int tiles_m, tiles_n, group_m;
   int binner;  // > 1: two-level batch (mdemi_gemm_desc.batch_inner)
   int64_t a_bs2, b_bs2, c_bs2;
+  const float* rowscale; FastDiv fd_rs;  // optional per-row-group scale before the residual add
+  // Tail split (batch 1): row tiles [0, tiles_m1) take the whole K; the tiles_m row tiles
+  // below m_split = tiles_m1 * BMT are split `split` ways (the last, partial round of
+  // tiles), as is every tile of an ordinary split-K GEMM (tiles_m1 = 0).
+  int tiles_m1, m_split;
+  int* tile_cnt;  // non-null: the last-arriving split of a tile combines the slabs (no reduce launch)
 };
 
 // element offset of batch entry b of an operand with outer stride s, inner stride s2
@@ -303,14 +309,15 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int 
   if (p.pre) p.pre[(int64_t)b * p.pre_bs + (int64_t)i * p.ldpre + j] = v;
   if (is_grad_act(p.act)) v *= aux_grad(p.act, p.aux[(int64_t)b * p.aux_bs + (int64_t)i * p.ldaux + j]);
   else if (p.act != MDEMI_ACT_NONE) v = apply_act(p.act, v);
+  if (p.rowscale) v *= p.rowscale[fdiv(i, p.fd_rs)];
   if (p.res) v += p.res[(int64_t)b * p.res_bs + (int64_t)i * p.ldres + j];
   return v;
 }
 
-// tile (tm, tn) for a linear workgroup id: XCD-aware remap (blocks b, b+8, ...
-// share an XCD), then grouped raster so concurrently running tiles of one XCD
-// reuse A row-panels (group_m rows of tiles) and B column-panels.
-__device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles, int& tm, int& tn) {
+// tile (tm, tn) for a linear workgroup id over tiles_m x tiles_n tiles: XCD-aware
+// remap (blocks b, b+8, ... share an XCD), then grouped raster so concurrently running
+// tiles of one XCD reuse A row-panels (group_m rows of tiles) and B column-panels.
+__device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles, int tiles_m, int& tm, int& tn) {
   if (p.group_m <= 0) {  // plain raster: n fastest
     tm = bid / p.tiles_n;
     tn = bid % p.tiles_n;
@@ -322,10 +329,38 @@ __device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles
   const int per_group = p.group_m * p.tiles_n;
   const int grp = lin / per_group;
   const int first_m = grp * p.group_m;
-  const int gm = min(p.tiles_m - first_m, p.group_m);
+  const int gm = min(tiles_m - first_m, p.group_m);
   const int in_grp = lin % per_group;
   tm = first_m + in_grp % gm;
   tn = in_grp / gm;
+}
+
+// What one workgroup computes: the whole-K tiles of the leading region come first in
+// launch order, then the split region's pieces (all tiles' piece 0, then piece 1, ...).
+struct GemmJob {
+  int b, sidx, tm, tn, cid;  // cid: counter slot of a split tile
+  bool split;
+};
+__device__ __forceinline__ GemmJob job_of(const GemmParams& p) {
+  GemmJob j;
+  const int n1 = p.tiles_m1 * p.tiles_n;
+  int bid = blockIdx.x;
+  if (bid < n1) {
+    j.b = 0; j.sidx = 0; j.split = false; j.cid = 0;
+    tile_of(p, bid, n1, p.tiles_m1, j.tm, j.tn);
+    return j;
+  }
+  bid -= n1;
+  const int n2 = p.tiles_m * p.tiles_n;
+  const int zb = bid / n2, t2 = bid - zb * n2;
+  j.b = zb / p.split;
+  j.sidx = zb - j.b * p.split;
+  j.split = p.split > 1;
+  int tm2;
+  tile_of(p, t2, n2, p.tiles_m, tm2, j.tn);
+  j.tm = p.tiles_m1 + tm2;
+  j.cid = j.b * n2 + tm2 * p.tiles_n + j.tn;
+  return j;
 }
 
 // precision modes of the GEMM entry points

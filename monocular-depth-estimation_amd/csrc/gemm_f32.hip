@@ -29,6 +29,8 @@
 #include "gemm_core.h"
 #include "gemm_f32_kernel.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -41,7 +43,7 @@ namespace mdemi {
 // partials [split][M] of a weight-gradient GEMM (bias gradient) in the same launch.
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const float* __restrict__ rs_part,
                                                           float* __restrict__ rs_out) {
-  const int64_t MN = (int64_t)p.M * p.N;
+  const int64_t MN = (int64_t)(p.M - p.m_split) * p.N;  // the split rows [m_split, M)
   const bool quad = (p.N & 3) == 0;
   const int64_t units = quad ? MN / 4 : MN;
   const int64_t total = units * p.batch;
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const fl
     const int b = (int)(e / units);
     const int64_t u = e - (int64_t)b * units;
     const int64_t rem = quad ? 4 * u : u;
-    const int i = (int)(rem / p.N), j = (int)(rem - (int64_t)i * p.N);
+    const int i = (int)(rem / p.N) + p.m_split, j = (int)(rem - (int64_t)(i - p.m_split) * p.N);
     const float* src = p.slab + (int64_t)b * MN + rem;
     float* dst = p.C + boff(p, b, p.c_bs, p.c_bs2) + (int64_t)i * p.ldc + j;
     if (quad) {
@@ -95,6 +97,14 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const fl
 // boundaries, so the choice never changes a result bit.
 constexpr int NVARIANTS = 8;
 static int g_variant = -1;  // -1: autotune per shape
+// A/B switches (environment, read once): MDEMI_GEMM_TAIL_SPLIT=0 disables the tail split,
+// MDEMI_GEMM_INLINE_REDUCE=0 combines split-K slabs with the separate reduce kernel.
+static bool env_on(const char* name) {
+  const char* v = getenv(name);
+  return !(v && v[0] == '0');
+}
+static bool g_tail_split = env_on("MDEMI_GEMM_TAIL_SPLIT");
+static bool g_inline_reduce = env_on("MDEMI_GEMM_INLINE_REDUCE");
 static int g_variant_m16 = -1;  // 16-bit family (bf16 / split fp32): 0 two LDS buffers, 1 one
 static int g_group_m = 8;
 
@@ -139,6 +149,9 @@ static int validate(const mdemi_gemm_desc* d) {
   MDEMI_REQUIRE(!d->rowsum_a || (d->a_layout == MDEMI_L_MNCONTIG && d->batch == 1),
                 "gemm: rowsum_a needs an m-contiguous A and batch 1");
   if (d->rowsum_a) MDEMI_REQUIRE(d->rowsum_a != d->C, "gemm: rowsum_a must not alias C");
+  if (d->row_scale)
+    MDEMI_REQUIRE(d->batch == 1 && d->row_scale_group > 0 && d->row_scale_group < ((int64_t)1 << 31),
+                  "gemm: row_scale needs batch 1 and 0 < row_scale_group < 2^31");
   if (d->batch_inner > 1)
     MDEMI_REQUIRE(d->batch % d->batch_inner == 0 && !d->aux && !d->residual && !d->preact && !d->rowsum_a,
                   "gemm: batch_inner needs batch %% batch_inner == 0 and no aux/residual/preact/rowsum_a");
@@ -151,6 +164,46 @@ static int validate(const mdemi_gemm_desc* d) {
   MDEMI_REQUIRE(!(d->act == MDEMI_ACT_GELU_GRAD || d->act == MDEMI_ACT_RELU_GRAD || d->act == MDEMI_ACT_SILU_GRAD) ||
                     d->aux, "gemm: *_GRAD epilogue needs aux");
   return MDEMI_OK;
+}
+
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    hipDeviceProp_t pr;
+    cus[dev] = hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0 ? pr.multiProcessorCount
+                                                                                           : 256;
+  }
+  return cus[dev];
+}
+
+// Tail split.  A whole-K GEMM whose 128x128 tiles fill R full rounds of resident
+// workgroups plus a thin last round (profiles/round3: 9600x3072x768 = 2.34 rounds of the
+// 3-workgroup/CU variant runs at 115 TF/s vs 130 at exactly 2 or 3 rounds) splits the rows
+// holding the leftover tiles into `split` K pieces, which fit in the last round's free
+// slots, and the last-arriving piece of each tile combines them.  The plan depends on the
+// shape only (rows cut at a 256-row boundary, K at the family's 32-element chunks), so every
+// variant splits the same outputs the same way and the family stays bit-identical.
+struct TailPlan {
+  int m_split, split;  // split 1: no tail split
+};
+static TailPlan tail_plan(const mdemi_gemm_desc* d) {
+  TailPlan t{0, 1};
+  if (!g_tail_split || d->split_k > 1 || d->batch != 1 || d->rowsum_a) return t;
+  const int64_t tm = cdiv(d->M, 128), tn = cdiv(d->N, 128), T = tm * tn;
+  const int64_t S = 3LL * device_cus();  // resident 128x128 tiles (3 workgroups per CU)
+  const int64_t full = T / S, rem = T - full * S;
+  if (full < 1 || rem == 0 || rem * 10 > S * 6) return t;  // no thin last round
+  const int64_t m_split = (tm - cdiv(rem, tn)) / 2 * 256;
+  if (m_split <= 0) return t;
+  const int64_t tail_tiles = cdiv(d->M - m_split, 128) * tn;
+  int64_t s = std::min<int64_t>(4, S / tail_tiles);
+  s = std::min<int64_t>(s, cdiv(d->K, 32) / 2);  // every piece keeps >= 2 K chunks
+  if (s < 2) return t;
+  t.m_split = (int)m_split;
+  t.split = (int)s;
+  return t;
 }
 
 static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, int mode) {
@@ -166,6 +219,8 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
   p.cv = d->conv;
   p.pre = d->preact; p.ldpre = d->ldpre; p.pre_bs = d->pre_bstride;
   p.rowsum = d->rowsum_a;
+  p.rowscale = d->row_scale;
+  if (d->row_scale) p.fd_rs = make_fastdiv((uint32_t)d->row_scale_group);
   p.binner = d->batch_inner > 1 ? d->batch_inner : 1;
   p.a_bs2 = p.binner > 1 ? d->a_bstride_inner : 0;
   p.b_bs2 = p.binner > 1 ? d->b_bstride_inner : 0;
@@ -174,10 +229,14 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
   // variants of a family agree bit for bit
   const int CH = 32;
   const int kc = (int)cdiv(d->K, CH);
-  const int split = d->split_k < kc ? d->split_k : kc;
+  const TailPlan tp = tail_plan(d);
+  const int want = tp.split > 1 ? tp.split : d->split_k;
+  const int split = want < kc ? want : kc;
   const int chunks_per_split = (int)cdiv(kc, split);
   p.ktile_per_split = chunks_per_split * (CH / GBK);
   p.split = (int)cdiv(kc, chunks_per_split);
+  p.m_split = (tp.split > 1 && p.split > 1) ? tp.m_split : 0;
+  p.tile_cnt = nullptr;
   // vector loads need every row start 16-B aligned and whole quads in range
   // (KCONTIG: K % 4; MNCONTIG: the row/column extent % 4)
   p.a_vec = al16(d->A) && (d->lda % 4 == 0) && (d->a_bstride % 4 == 0) && (p.a_bs2 % 4 == 0) &&
@@ -190,7 +249,9 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
     p.fd_ow = make_fastdiv(g.ow); p.fd_oh = make_fastdiv(g.oh);
   }
   p.slab = nullptr;
-  p.tiles_m = (int)cdiv(d->M, variant_rows(variant, mode));  // 256-row variants: 16-bit 2, fp32 6 and 7
+  const int vrows = variant_rows(variant, mode);  // 256-row variants: 16-bit 2, fp32 6 and 7
+  p.tiles_m1 = p.m_split / vrows;
+  p.tiles_m = (int)cdiv(d->M - p.m_split, vrows);
   p.tiles_n = (int)cdiv(d->N, GBN);
   p.group_m = g_group_m;
 }
@@ -200,7 +261,32 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
 using namespace mdemi;
 
 static size_t slab_bytes(const mdemi_gemm_desc* d, const GemmParams& p) {
-  return p.split > 1 ? align_up((size_t)p.split * d->batch * (size_t)d->M * d->N * sizeof(float), 256) : 0;
+  return p.split > 1 ? align_up((size_t)p.split * d->batch * (size_t)(d->M - p.m_split) * d->N * sizeof(float), 256)
+                     : 0;
+}
+
+// Per-device split-tile counters for the in-kernel slab combine: zeroed once on the
+// launch stream, left zeroed by every launch (the last arriver resets its tile's slot).
+// GEMMs with split tiles on two streams at once would share them: the library runs its
+// GEMMs on one compute stream.  None is allocated during a graph capture (nullptr: the
+// launch falls back to the reduce kernel); a grown buffer keeps the old one alive for
+// graphs that recorded it.
+static int* tile_counters(int64_t n, hipStream_t st) {
+  static std::mutex mu;
+  static std::map<int, std::pair<int*, int64_t>> bufs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = bufs[dev];
+  if (e.second >= n) return e.first;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  const int64_t cap = std::max<int64_t>(n, (int64_t)1 << 16);
+  int* ptr = nullptr;
+  if (hipMalloc(&ptr, cap * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(ptr, 0, cap * sizeof(int), st) != hipSuccess) return nullptr;
+  e = {ptr, cap};
+  return ptr;
 }
 static size_t rowsum_bytes(const mdemi_gemm_desc* d, const GemmParams& p) {
   return (p.split > 1 && d->rowsum_a) ? (size_t)p.split * d->M * sizeof(float) : 0;
@@ -239,11 +325,14 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mod
       p.rowsum = rowsum_part;
     }
   }
-  const int64_t nblocks = (int64_t)p.tiles_m * p.tiles_n * d->batch * p.split;
+  const int64_t nblocks = (int64_t)p.tiles_m1 * p.tiles_n + (int64_t)p.tiles_m * p.tiles_n * d->batch * p.split;
   MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
+  const bool deep = p.split > 1 && colsum_combine(d, p);
+  if (p.split > 1 && !deep && !rowsum_part && (g_inline_reduce || p.m_split > 0))
+    p.tile_cnt = tile_counters((int64_t)p.tiles_m * p.tiles_n * d->batch, st);
   hipLaunchKernelGGL(fn, dim3((unsigned)nblocks), dim3(GTHREADS), 0, st, p);
-  if (p.split > 1) {
-    if (colsum_combine(d, p)) {
+  if (p.split > 1 && !p.tile_cnt) {
+    if (deep) {
       // many slabs over a small C (skinny weight gradients over ~10^6 pixels): a
       // column sum parallel over the slab rows, not one thread per output summing
       // `split` dependent loads
@@ -252,7 +341,7 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mod
       if (!rc && rowsum_part) rc = colsum_launch(rowsum_part, p.split, d->M, d->M, d->rowsum_a, 0, cws, st);
       if (rc) return rc;
     } else {
-      const int64_t total = (int64_t)d->M * d->N * d->batch / ((d->N & 3) == 0 ? 4 : 1);
+      const int64_t total = (int64_t)(d->M - p.m_split) * d->N * d->batch / ((d->N & 3) == 0 ? 4 : 1);
       const int nb = (int)(cdiv(total, 256) < 4096 ? cdiv(total, 256) : 4096);
       hipLaunchKernelGGL(gemm_splitk_reduce, dim3(nb), dim3(256), 0, st, p, (const float*)rowsum_part,
                          rowsum_part ? d->rowsum_a : (float*)nullptr);
@@ -317,7 +406,7 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
 }
 
 extern "C" size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d) {
-  if (!d || d->split_k <= 1) return 0;
+  if (!d) return 0;
   GemmParams p;
   fill_params(d, p, 0, GEMM_F32);  // every family splits at the same 32-element chunks
   if (p.split <= 1) return 0;
@@ -343,6 +432,12 @@ extern "C" int mdemi_gemm_set_variant(int32_t variant, int32_t group_m) {
   MDEMI_REQUIRE(variant >= -1 && variant < NVARIANTS && group_m >= 0, "gemm_set_variant: bad args");
   g_variant = variant;
   g_group_m = group_m;
+  return MDEMI_OK;
+}
+
+extern "C" int mdemi_gemm_set_options(int32_t tail_split, int32_t inline_reduce) {
+  g_tail_split = tail_split != 0;
+  g_inline_reduce = inline_reduce != 0;
   return MDEMI_OK;
 }
 

@@ -31,11 +31,8 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int ntiles = p.tiles_m * p.tiles_n;
-  const int zb = blockIdx.x / ntiles;
-  int tm, tn;
-  tile_of(p, blockIdx.x % ntiles, ntiles, tm, tn);
-  const int b = zb / p.split, sidx = zb % p.split;
+  const GemmJob job = job_of(p);
+  const int b = job.b, sidx = job.sidx, tm = job.tm, tn = job.tn;
   const int bm = tm * BMT, bn = tn * GBN;
 
   LA la[NA];
@@ -46,8 +43,8 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   lb.init(p.B + boff(p, b, p.b_bs, p.b_bs2), p.ldb, p.N, p.K, p.b_vec, bn, t, p);
 
   const int ktiles_total = (p.K + BK - 1) / BK;
-  const int kt_begin = sidx * p.ktile_per_split;
-  const int kt_end = min(ktiles_total, kt_begin + p.ktile_per_split);
+  const int kt_begin = job.split ? sidx * p.ktile_per_split : 0;
+  const int kt_end = job.split ? min(ktiles_total, kt_begin + p.ktile_per_split) : ktiles_total;
 
   floatx16 acc[IM][2];
 #pragma unroll
@@ -187,7 +184,7 @@ static KernelFn pick_variant(int v) {
     case 1: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, false, 2>;
     case 2: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 4>;
     case 3: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, true, 2>;
-    case 4: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 1, true, true, 2>;
+    case 4: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 1, true, true, 3>;
     case 5: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, false, 2>;
     case 6: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 1, true, true, 2, 256>;
     case 7: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 2, 256>;

@@ -64,6 +64,7 @@ class GemmDesc(ctypes.Structure):
         ("rowsum_a", vp),
         ("batch_inner", i32), ("_pad1", i32),
         ("a_bstride_inner", i64), ("b_bstride_inner", i64), ("c_bstride_inner", i64),
+        ("row_scale", vp), ("row_scale_group", i64),
     ]
 
 
@@ -117,6 +118,7 @@ _SIGS = {
     "mdemi_gemm_f32e": (ctypes.c_int, [ctypes.POINTER(GemmDesc), vp]),
     "mdemi_gemm_set_variant": (ctypes.c_int, [i32, i32]),
     "mdemi_gemm_set_variant_m16": (ctypes.c_int, [i32]),
+    "mdemi_gemm_set_options": (ctypes.c_int, [i32, i32]),
     "mdemi_colsum_workspace_size": (sz, [i64, i64]),
     "mdemi_colsum_f32": (ctypes.c_int, [vp, i64, i64, i64, vp, ctypes.c_int, vp, vp]),
     "mdemi_headconv_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),

@@ -107,7 +107,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
          res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0, rowsum_a=None,
-         a_off=0, b_off=0, c_off=0, inner=None):
+         a_off=0, b_off=0, c_off=0, inner=None, row_scale=None, row_scale_group=0):
     """a_off/b_off/c_off: element offsets into A/B/C (column slices of wider buffers).
     inner=(n, a_bstride_inner, b_bstride_inner, c_bstride_inner): a two-level batch of
     batch = outer * n entries (mdemi_gemm_desc.batch_inner), e.g. (image, head)."""
@@ -138,6 +138,8 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
         d.preact, d.ldpre, d.pre_bstride = preact.data_ptr(), ldpre, pre_bstride
     if rowsum_a is not None:
         d.rowsum_a = rowsum_a.data_ptr()
+    if row_scale is not None:
+        d.row_scale, d.row_scale_group = row_scale.data_ptr(), row_scale_group
     lib = L.load()
     need = lib.mdemi_gemm_workspace_size(ctypes.byref(d))
     if need:
@@ -168,7 +170,9 @@ def colsum(x2d, out=None, accumulate=False):
 # --------------------------------------------------------------------------
 
 
-def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NONE, out=None):
+def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NONE, out=None, drop_scale=None):
+    """drop_scale: per-sample DropPath scale [B] of the product (rows grouped M / B per sample),
+    applied in the epilogue before the residual add."""
     M, K = x2.shape
     N = weight.shape[0]
     if out is None:
@@ -176,19 +180,29 @@ def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NON
     gemm(x2, weight, out, M, N, K, lda=K, ldb=K, ldc=out.stride(0), a_layout=L.L_KCONTIG,
          b_layout=L.L_KCONTIG, a_op=L.OP_GELU if in_gelu else L.OP_NONE,
          bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act,
-         residual=residual, ldres=(residual.stride(0) if residual is not None else 0), split_k=1)
+         residual=residual, ldres=(residual.stride(0) if residual is not None else 0), split_k=1,
+         row_scale=drop_scale, row_scale_group=(M // drop_scale.numel() if drop_scale is not None else 0))
     return out
+
+
+def _drop_rows(dy2, scale):
+    """s[sample] * dy: the DropPath branch gradient (rows grouped per sample)."""
+    db = torch.empty_like(dy2)
+    L.call("mdemi_rowscale_add", None, dy2.data_ptr(), scale.data_ptr(), db.data_ptr(), dy2.numel() // scale.numel(),
+           dy2.numel(), L.stream())
+    return db
 
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, in_gelu):
+    def forward(ctx, x, weight, bias, residual, in_gelu, drop_scale):
         _require_cuda(x, weight, bias, residual)
         K = x.shape[-1]
         x2 = _c(x).reshape(-1, K)
         res2 = _c(residual).reshape(x2.shape[0], -1) if residual is not None else None
-        out = linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2)
+        out = linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2, drop_scale=drop_scale)
         ctx.save_for_backward(x2, weight)
+        ctx.drop_scale = drop_scale
         ctx.in_gelu = in_gelu
         ctx.has_bias = bias is not None
         ctx.has_res = residual is not None
@@ -201,6 +215,8 @@ class _LinearFn(torch.autograd.Function):
         M, K = x2.shape
         N = weight.shape[0]
         dy2 = _c(dy).reshape(M, N)
+        if ctx.drop_scale is not None:  # the branch's gradient; the residual's stays dy
+            dy2 = _drop_rows(dy2, ctx.drop_scale)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, device=dy.device, dtype=torch.float32)
@@ -220,12 +236,15 @@ class _LinearFn(torch.autograd.Function):
         elif want_db:
             colsum(dy2, out=db)
         dres = dy if ctx.has_res and ctx.needs_input_grad[3] else None
-        return dx, dw, db, dres, None
+        return dx, dw, db, dres, None, None
 
 
-def linear(x, weight, bias=None, residual=None, in_gelu=False):
-    """y = (gelu(x) if in_gelu else x) @ W^T + b (+ residual)."""
-    return _LinearFn.apply(x, weight, bias, residual, in_gelu)
+def linear(x, weight, bias=None, residual=None, in_gelu=False, drop_scale=None):
+    """y = (gelu(x) if in_gelu else x) @ W^T + b (+ residual); drop_scale (DropPath, per
+    sample [B]): y = residual + drop_scale[sample] * (x @ W^T + b), fused in the epilogue."""
+    if drop_scale is not None and residual is None:
+        raise ValueError("linear: drop_scale scales a residual branch and needs residual")
+    return _LinearFn.apply(x, weight, bias, residual, in_gelu, drop_scale)
 
 
 class _MlpFn(torch.autograd.Function):
@@ -241,7 +260,7 @@ class _MlpFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, residual, cfg):
-        act, p_mid, p_out, seed = cfg
+        act, p_mid, p_out, seed, drop_scale = cfg
         _require_cuda(x, w1, b1, w2, b2, residual)
         K = x.shape[-1]
         x2 = _c(x).reshape(-1, K)
@@ -262,7 +281,7 @@ class _MlpFn(torch.autograd.Function):
                 L.call("mdemi_elementwise", L.EW_ADD, out.data_ptr(), res2.data_ptr(), out.data_ptr(), out.numel(),
                        0.0, 0.0, L.stream())
         else:
-            out = linear_fwd_raw(g, _c(w2), b2, residual=res2)
+            out = linear_fwd_raw(g, _c(w2), b2, residual=res2, drop_scale=drop_scale)
         ctx.save_for_backward(x2, w1, w2, h, g)
         ctx.flags = (b1 is not None, b2 is not None, residual is not None)
         ctx.cfg = cfg
@@ -273,10 +292,12 @@ class _MlpFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w1, w2, h, g = ctx.saved_tensors
         has_b1, has_b2, has_res = ctx.flags
-        act, p_mid, p_out, seed = ctx.cfg
+        act, p_mid, p_out, seed, drop_scale = ctx.cfg
         M, K = x2.shape
         Hd, N = w1.shape[0], w2.shape[0]
         dy2 = _c(dy).reshape(M, N)
+        if drop_scale is not None:  # the branch's gradient; the residual's stays dy
+            dy2 = _drop_rows(dy2, drop_scale)
         dev = dy.device
         if p_out > 0.0:
             d2 = torch.empty_like(dy2)
@@ -310,12 +331,16 @@ class _MlpFn(torch.autograd.Function):
         return dx, dw1, db1, dw2, db2, dres, None
 
 
-def mlp(x, w1, b1, w2, b2, residual=None, act=L.ACT_GELU, p_mid=0.0, p_out=0.0, training=False):
-    """fc2(dropout(act(fc1(x)))) -> dropout (+ residual); act GELU (exact erf), SiLU or ReLU."""
+def mlp(x, w1, b1, w2, b2, residual=None, act=L.ACT_GELU, p_mid=0.0, p_out=0.0, training=False, drop_scale=None):
+    """fc2(dropout(act(fc1(x)))) -> dropout (+ residual); act GELU (exact erf), SiLU or ReLU.
+    drop_scale (DropPath, per sample [B]): residual + drop_scale[sample] * branch, fused in
+    fc2's epilogue (no output dropout with it)."""
     if not training:
         p_mid = p_out = 0.0
+    if drop_scale is not None and (residual is None or p_out > 0.0):
+        raise ValueError("mlp: drop_scale needs a residual and no output dropout")
     seed = _draw_seed(x.device) if (p_mid > 0.0 or p_out > 0.0) else None
-    return _MlpFn.apply(x, w1, b1, w2, b2, residual, (act, float(p_mid), float(p_out), seed))
+    return _MlpFn.apply(x, w1, b1, w2, b2, residual, (act, float(p_mid), float(p_out), seed, drop_scale))
 
 
 # --------------------------------------------------------------------------
@@ -1106,12 +1131,16 @@ class _DropPathAddFn(torch.autograd.Function):
         return dy, db, None
 
 
+def drop_path_scale(batch, drop_prob, device):
+    """timm DropPath's per-sample scale: bernoulli(keep) / keep, drawn on the device."""
+    keep = 1.0 - drop_prob
+    return torch.empty(batch, device=device, dtype=torch.float32).bernoulli_(keep).div_(keep)
+
+
 def drop_path_add(res, branch, drop_prob, training):
     if drop_prob == 0.0 or not training:
         return add(res, branch)
-    keep = 1.0 - drop_prob
-    scale = torch.empty(branch.shape[0], device=branch.device, dtype=torch.float32).bernoulli_(keep).div_(keep)
-    return _DropPathAddFn.apply(res, branch, scale)
+    return _DropPathAddFn.apply(res, branch, drop_path_scale(branch.shape[0], drop_prob, branch.device))
 
 
 def batch_norm_eval_nhwc(x, weight, bias, running_mean, running_var, eps=1e-5, act=L.ACT_NONE):

@@ -43,8 +43,9 @@ class Mlp(nn.Module):
         if not isinstance(self.act, nn.GELU):
             raise ValueError("Mlp: only the reference's nn.GELU activation is built")
 
-    def forward(self, x, residual=None):
-        return mf.mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual=residual)
+    def forward(self, x, residual=None, drop_scale=None):
+        return mf.mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual=residual,
+                      drop_scale=drop_scale)
 
 
 class WindowAttention(nn.Module):
@@ -109,12 +110,12 @@ class SwinTransformerBlock(nn.Module):
             x2 = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x2)
             xn, x2 = mf.layer_norm_skip(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps)
             x2 = self.mlp(xn, residual=x2)
-        else:
-            br = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias)
-            x2 = mf.drop_path_add(x2.view(B, -1), br.view(B, -1), p, True).view(B * Lq, C)
+        else:  # DropPath (swin_transformer.py:232,239): the per-sample scale rides in the proj / fc2 epilogues
+            s1 = mf.drop_path_scale(B, p, x.device)
+            x2 = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x2, drop_scale=s1)
             xn, x2 = mf.layer_norm_skip(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps)
-            br = self.mlp(xn)
-            x2 = mf.drop_path_add(x2.view(B, -1), br.view(B, -1), p, True).view(B * Lq, C)
+            s2 = mf.drop_path_scale(B, p, x.device)
+            x2 = self.mlp(xn, residual=x2, drop_scale=s2)
         return x2.view(B, Lq, C)
 
 

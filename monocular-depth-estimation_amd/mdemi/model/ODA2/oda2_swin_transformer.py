@@ -47,10 +47,10 @@ class SwinMLP(nn.Module):
         if not isinstance(self.act, nn.GELU):
             raise ValueError("SwinMLP: only the reference's nn.GELU is built")
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, drop_scale=None):
         p = self.drop.p
         return mf.mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual=residual,
-                      p_mid=p, p_out=p, training=self.training)
+                      p_mid=p, p_out=p, training=self.training, drop_scale=drop_scale)
 
 
 class SwinWindowing(nn.Module):
@@ -155,12 +155,15 @@ class SwinTransformerBlock(nn.Module):
             x2 = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x2)
             xn, x2 = mf.layer_norm_skip(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps)
             x2 = self.mlp(xn, residual=x2)
-        else:
-            br = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias)
-            x2 = mf.drop_path_add(x2.view(b, -1), br.view(b, -1), p, True).view(b * n, c)
+        else:  # DropPath: the per-sample scale rides in the proj / fc2 epilogues
+            s1 = mf.drop_path_scale(b, p, x.device)
+            x2 = mf.linear(a, self.attn.proj.weight, self.attn.proj.bias, residual=x2, drop_scale=s1)
             xn, x2 = mf.layer_norm_skip(x2, self.norm2.weight, self.norm2.bias, self.norm2.eps)
-            br = self.mlp(xn)
-            x2 = mf.drop_path_add(x2.view(b, -1), br.view(b, -1), p, True).view(b * n, c)
+            if self.mlp.drop.p > 0.0:  # output dropout sits between fc2 and the scale: unfused
+                br = self.mlp(xn)
+                x2 = mf.drop_path_add(x2.view(b, -1), br.view(b, -1), p, True).view(b * n, c)
+            else:
+                x2 = self.mlp(xn, residual=x2, drop_scale=mf.drop_path_scale(b, p, x.device))
         return x2.view(b, n, c)
 
 

@@ -6,6 +6,23 @@ torch.hub download in the reference (unet_adaptive_bins.py:129): parity unpinned
 import torch
 import torch.nn.functional as F
 
+# Test hook (kink-aware comparisons): when set to a list of boolean tensors, every
+# ReLU / LeakyReLU of the head takes its branch from the next mask in call order
+# (mask = "pre-activation > 0" as the GPU forward decided it) instead of from the sign
+# of its own input, so the oracle differentiates the same piecewise-linear function as
+# the GPU even where an fp32 rounding put a pre-activation on the other side of the kink.
+KINK = None
+
+
+def _kink_act(x, slope):
+    """F.relu (slope 0) / F.leaky_relu (slope 0.01), or the KINK-masked branch."""
+    global KINK
+    if KINK is not None:
+        m = KINK.pop(0).to(x.device)
+        assert m.shape == x.shape, (m.shape, x.shape)
+        return torch.where(m, x, x * slope)
+    return F.leaky_relu(x, slope) if slope else F.relu(x)
+
 
 def bn_train(P, pre, x, eps=1e-5):
     return F.batch_norm(x, None, None, P[pre + "weight"], P[pre + "bias"], training=True, eps=eps)
@@ -14,10 +31,10 @@ def bn_train(P, pre, x, eps=1e-5):
 def upsample_bn(P, pre, x, concat_with):  # unet_adaptive_bins.py:8-24
     up_x = F.interpolate(x, size=[concat_with.size(2), concat_with.size(3)], mode="bilinear", align_corners=True)
     f = torch.cat([up_x, concat_with], dim=1)
-    f = F.leaky_relu(bn_train(P, pre + "_net.1.", F.conv2d(f, P[pre + "_net.0.weight"], P[pre + "_net.0.bias"],
-                                                            padding=1)))
-    return F.leaky_relu(bn_train(P, pre + "_net.4.", F.conv2d(f, P[pre + "_net.3.weight"], P[pre + "_net.3.bias"],
-                                                               padding=1)))
+    f = _kink_act(bn_train(P, pre + "_net.1.", F.conv2d(f, P[pre + "_net.0.weight"], P[pre + "_net.0.bias"],
+                                                         padding=1)), 0.01)
+    return _kink_act(bn_train(P, pre + "_net.4.", F.conv2d(f, P[pre + "_net.3.weight"], P[pre + "_net.3.bias"],
+                                                            padding=1)), 0.01)
 
 
 def decoder_bn(P, pre, features):  # unet_adaptive_bins.py:27-57
@@ -45,7 +62,7 @@ def transformer_encoder_layer(P, pre, src, heads):
     o = (attn @ v).transpose(0, 1).contiguous().view(S, N, E)
     o = F.linear(o, P[pre + "self_attn.out_proj.weight"], P[pre + "self_attn.out_proj.bias"])
     x = F.layer_norm(src + o, (E,), P[pre + "norm1.weight"], P[pre + "norm1.bias"], 1e-5)
-    ff = F.linear(F.relu(F.linear(x, P[pre + "linear1.weight"], P[pre + "linear1.bias"])),
+    ff = F.linear(_kink_act(F.linear(x, P[pre + "linear1.weight"], P[pre + "linear1.bias"]), 0.0),
                   P[pre + "linear2.weight"], P[pre + "linear2.bias"])
     return F.layer_norm(x + ff, (E,), P[pre + "norm2.weight"], P[pre + "norm2.bias"], 1e-5)
 
@@ -71,11 +88,11 @@ def mvit(P, pre, x, n_query_channels=128, patch_size=16, norm="linear"):  # mini
     x = F.conv2d(x, P[pre + "embedding_conv.weight"], P[pre + "embedding_conv.bias"], padding=1)
     head, queries = tgt[0, ...], tgt[1:n_query_channels + 1, ...]
     range_maps = pixel_wise_dot(x, queries.permute(1, 0, 2))
-    y = F.leaky_relu(F.linear(head, P[pre + "regressor.0.weight"], P[pre + "regressor.0.bias"]))
-    y = F.leaky_relu(F.linear(y, P[pre + "regressor.2.weight"], P[pre + "regressor.2.bias"]))
+    y = _kink_act(F.linear(head, P[pre + "regressor.0.weight"], P[pre + "regressor.0.bias"]), 0.01)
+    y = _kink_act(F.linear(y, P[pre + "regressor.2.weight"], P[pre + "regressor.2.bias"]), 0.01)
     y = F.linear(y, P[pre + "regressor.4.weight"], P[pre + "regressor.4.bias"])
     if norm == "linear":
-        y = torch.relu(y) + 0.1
+        y = _kink_act(y, 0.0) + 0.1
     elif norm == "softmax":
         return torch.softmax(y, dim=1), range_maps
     else:

@@ -577,6 +577,113 @@ def test_gemm_variants_bit_identical(mf, layouts):
         assert torch.equal(c, same), f"variant {v} split {split} differs bitwise"
 
 
+@pytest.mark.parametrize("layouts", ["fwd", "dgrad"])
+def test_gemm_tail_split(mf, layouts):
+    """Tail split (gemm_f32.hip tail_plan): 9600x3072x768 leaves a thin third round of
+    128x128 tiles, so the rows holding them are cut at a 256-row boundary and split over K
+    (combined by the last-arriving piece).  Every variant must agree bit for bit with the
+    split on; rows above the cut equal the unsplit result bit for bit; all within the fp32
+    bound of an fp64 product; the fused epilogue (bias, residual) runs after the combine."""
+    from mdemi import _lib as L
+    lib = L.load()
+    M, N, K = 9600, 3072, 768
+    g = torch.Generator(device=DEV).manual_seed(5)
+    a = torch.randn(M, K, device=DEV, generator=g)
+    b = torch.randn(N, K, device=DEV, generator=g)
+    bt = b.t().contiguous()
+    bias = torch.randn(N, device=DEV, generator=g)
+    res = torch.randn(M, N, device=DEV, generator=g)
+
+    def run(v, tail):
+        L.check(lib.mdemi_gemm_set_variant(v, 8), "set_variant")
+        L.check(lib.mdemi_gemm_set_options(tail, 1), "set_options")
+        c = torch.empty(M, N, device=DEV)
+        if layouts == "fwd":
+            mf.gemm(a, b, c, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG, split_k=1,
+                    bias=bias, bias_mode=L.BIAS_COL, residual=res, ldres=N)
+        else:
+            mf.gemm(a, bt, c, M, N, K, lda=K, ldb=N, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG, split_k=1,
+                    bias=bias, bias_mode=L.BIAS_COL, residual=res, ldres=N)
+        return c
+
+    try:
+        plain = run(4, 0)
+        outs = [(v, run(v, 1)) for v in (0, 1, 3, 4, 5, 6, 7)]
+    finally:
+        lib.mdemi_gemm_set_variant(-1, 8)
+        lib.mdemi_gemm_set_options(1, 1)
+    ref = (a.double() @ b.double().t() + bias.double() + res.double()).float()
+    close(plain, ref, rtol=1e-5 * math.sqrt(K))
+    m_split = 8192  # (75 - ceil(264 / 24)) // 2 * 256 on a 256-CU device
+    for v, c in outs:
+        close(c, ref, rtol=1e-5 * math.sqrt(K))
+        assert torch.equal(c, outs[0][1]), f"variant {v} differs bitwise with the tail split"
+    c = outs[0][1]
+    assert torch.equal(c[:m_split], plain[:m_split]), "rows above the cut must be the unsplit result"
+    assert not torch.equal(c[m_split:], plain[m_split:]), "tail rows were not split (plan did not engage)"
+
+
+@pytest.mark.parametrize("layouts", ["fwd", "wgrad"])
+def test_gemm_inline_combine_matches_reduce_kernel(mf, layouts):
+    """Split-K slabs combined by the last-arriving piece of each tile (in split order) equal
+    the separate gemm_splitk_reduce launch bit for bit, and repeated launches reuse the
+    self-resetting tile counters."""
+    from mdemi import _lib as L
+    lib = L.load()
+    M, N, K = 700, 300, 5000
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(N, K, device=DEV)
+    at, bt = a.t().contiguous(), b.t().contiguous()
+
+    def run(inline):
+        L.check(lib.mdemi_gemm_set_options(1, inline), "set_options")
+        c = torch.empty(M, N, device=DEV)
+        if layouts == "fwd":
+            mf.gemm(a, b, c, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG, split_k=6)
+        else:
+            mf.gemm(at, bt, c, M, N, K, lda=M, ldb=N, ldc=N, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+                    split_k=6)
+        return c
+
+    try:
+        k = run(0)
+        outs = [run(1) for _ in range(3)]
+    finally:
+        lib.mdemi_gemm_set_options(1, 1)
+    close(k, (a.double() @ b.double().t()).float(), rtol=1e-5 * math.sqrt(K))
+    for c in outs:
+        assert torch.equal(c, k)
+
+
+def test_linear_and_mlp_drop_scale(mf):
+    """DropPath fused into the proj / fc2 epilogue: y = res + s[sample] * (x W^T + b), and the
+    branch gradients see s * dy while the residual's gradient is dy."""
+    B, Lq, C, Hd = 3, 50, 64, 256
+    x = rnd(B * Lq, C, seed=120)
+    res = rnd(B * Lq, C, seed=121)
+    w, bb = rnd(C, C, seed=122, scale=0.2), rnd(C, seed=123)
+    w1, b1, w2, b2 = rnd(Hd, C, seed=124, scale=0.2), rnd(Hd, seed=125), rnd(C, Hd, seed=126, scale=0.1), rnd(C, seed=127)
+    s = torch.tensor([2.0, 0.0, 2.0], dtype=torch.float64)
+    srow = s.repeat_interleave(Lq).unsqueeze(1)
+    dy = rnd(B * Lq, C, seed=128)
+    # reference
+    xr, rr = x.clone().requires_grad_(), res.clone().requires_grad_()
+    wr, br_, w1r, b1r, w2r, b2r = (t.clone().requires_grad_() for t in (w, bb, w1, b1, w2, b2))
+    y1 = rr + srow * (xr @ wr.t() + br_)
+    y2 = y1 + srow * (F.gelu(y1 @ w1r.t() + b1r) @ w2r.t() + b2r)
+    y2.backward(dy)
+    # GPU
+    g = lambda t: t.float().to(DEV).requires_grad_()
+    xg, rg, wg, bg, w1g, b1g, w2g, b2g = (g(t) for t in (x, res, w, bb, w1, b1, w2, b2))
+    sg = s.float().to(DEV)
+    z1 = mf.linear(xg, wg, bg, residual=rg, drop_scale=sg)
+    z2 = mf.mlp(z1, w1g, b1g, w2g, b2g, residual=z1, drop_scale=sg)
+    z2.backward(dy.float().to(DEV))
+    close(z2, y2, rtol=1e-5)
+    for got, ref in ((xg, xr), (rg, rr), (wg, wr), (bg, br_), (w1g, w1r), (b1g, b1r), (w2g, w2r), (b2g, b2r)):
+        close(got.grad, ref.grad, rtol=1e-4)
+
+
 @pytest.mark.parametrize("cout,cin,kh,kw", [(8, 12, 3, 3), (5, 7, 5, 5), (16, 3, 4, 4), (6, 10, 1, 1), (4, 4, 1, 3)])
 def test_conv_weight_layout(cout, cin, kh, kw):
     """mdemi_conv_weight_layout against the torch permutations it replaces (bit-exact)."""
