@@ -392,7 +392,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int r = 0; r < 16; ++r) dp[a][b][r] = 0.f;
     mma_hd(dp, vf, df);  // dP^T[key][q] = sum_d V[key][d] dO[q][d]
   }
-  wave_lds_sync();  // tabg, pads, regs
+  wave_lds_sync();  // tabg, pads, regs, rowtab
+  // Column operands of the three products over the score tiles are fetched one phase
+  // ahead (each is a burst of per-lane L2 loads): dO columns now, land under the
+  // softmax-gradient pass; K columns before dV's MFMAs; Q columns before dQ's.
+  float dc[25];
+#pragma unroll
+  for (int j = 0; j < 25; ++j) dc[j] = col_val(p.dout, p.out_ld, nullptr, rowtab[wv][2 * j + h], col0 + l31);
   {
     float lse[2];
     int bq[2];
@@ -454,28 +460,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
   };
   // dV[key][d] = sum_q P^T[key][q] dO[q][d]
+  float kc[2][16];
   {
-    float dc[25];
-#pragma unroll
-    for (int j = 0; j < 25; ++j) {
-      dc[j] = col_val(p.dout, p.out_ld, nullptr, rowtab[wv][2 * j + h], col0 + l31);
-    }
     to_lds(s);
     wave_lds_sync();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) kc[t][r] = col_val(p.k, p.qk_ld, p.k_pad, rowtab[wv][t * 32 + acc_row(r, h)], col0 + l31);
     key_side(dc, p.dv, p.dv_ld, padv[wv]);
   }
   wave_lds_sync();  // every P^T read done
   to_lds(dp);
   wave_lds_sync();
+  float qc[25];
+#pragma unroll
+  for (int j = 0; j < 25; ++j) qc[j] = p.scale * col_val(p.q, p.qk_ld, p.q_pad, rowtab[wv][2 * j + h], col0 + l31);
   // dQ^T[d][q] = sum_key K[key][d] dS^T[key][q]  (K columns from global, dS^T from LDS)
   {
-    float kc[2][16];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        kc[t][r] = col_val(p.k, p.qk_ld, p.k_pad, rowtab[wv][t * 32 + acc_row(r, h)], col0 + l31);
-      }
     wa_f16x dq[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n)
@@ -502,14 +504,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   }
   // dK[key][d] = sum_q dS^T[key][q] (scale Q)[q][d]
-  {
-    float qc[25];
-#pragma unroll
-    for (int j = 0; j < 25; ++j) {
-      qc[j] = p.scale * col_val(p.q, p.qk_ld, p.q_pad, rowtab[wv][2 * j + h], col0 + l31);
-    }
-    key_side(qc, p.dk, p.dqk_ld, padk[wv]);
-  }
+  key_side(qc, p.dk, p.dqk_ld, padk[wv]);
   wave_lds_sync();  // tabg, pads complete
   if (it.active) {
     float* P = p.partial + (int64_t)it.item * (WA_T + 2 * HD);

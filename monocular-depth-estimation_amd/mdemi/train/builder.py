@@ -38,6 +38,8 @@ from __future__ import annotations
 
 import math
 
+import time
+
 import torch
 import torch.nn as nn
 
@@ -158,6 +160,10 @@ def freeze_bn(model):
             m.eval()
 
 
+# ProcessGroupNCCL's watchdog polls outstanding works every 100 ms (kWatchdogThreadSleepMillis)
+_WATCHDOG_RETIRE_S = 0.5
+
+
 class Trainer:
     """One optimizer step = num_accum micro-batches of forward + loss/num_accum + backward
     (gradients accumulate in place), then the gradient all-reduce (DDP), the clipped
@@ -234,12 +240,14 @@ class Trainer:
             self._static = [(img.clone(), gt.clone()) for img, gt in batches]
             self._zero_grad(set_to_none=False)
             if self.ddp is not None:
-                torch.cuda.synchronize()  # no collective of the eager steps may still be in flight
+                # No collective of the eager steps may still be in flight, and the process
+                # group's watchdog thread must have retired them: it polls each outstanding
+                # work's HIP event, which a global-mode capture refuses (it aborts the
+                # process).  Captured collectives are never handed to the watchdog.
+                torch.cuda.synchronize()
+                time.sleep(_WATCHDOG_RETIRE_S)
             g = torch.cuda.CUDAGraph()
-            # thread_local: only this thread's capture-unsafe calls are refused -- the RCCL
-            # process group's watchdog thread keeps polling the events of the eager steps'
-            # collectives while we capture (global mode fails its hipEventQuery)
-            with torch.cuda.graph(g, capture_error_mode="thread_local"), mf.matmul_precision(self.precision):
+            with torch.cuda.graph(g), mf.matmul_precision(self.precision):
                 self._static_loss = self._body(self._static)
                 self._zero_grad(set_to_none=False)  # gradients keep their (captured) addresses
             self._graph = g
