@@ -77,6 +77,10 @@ __device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
 __device__ __forceinline__ float buf_ld1(__amdgpu_buffer_rsrc_t r, int off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+// sc1 load (bypasses this CU's L1): reads bytes another workgroup stored sc1 in this launch
+__device__ __forceinline__ float buf_ld1_sc1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
 
 // n / d for 0 <= n < 2^31 by multiply-shift (host-computed magic, exact).
 __device__ __forceinline__ int fdiv(int n, const FastDiv& f) {

@@ -268,7 +268,10 @@ def _filled_state(model, seed, scale):
 
 
 def _oracle_run(sd, dtype, loss_fn):
-    P = {k: (v.to(dtype).requires_grad_(True) if torch.is_floating_point(v) else v) for k, v in sd.items()}
+    # fresh leaves every run (a no-op .to() would hand out sd's own tensors, whose .grad then
+    # accumulates across runs and turns later casts into non-leaves)
+    P = {k: (v.detach().to(dtype).clone().requires_grad_(True) if torch.is_floating_point(v) else v)
+         for k, v in sd.items()}
     outs = loss_fn(P)
     return P, outs
 
