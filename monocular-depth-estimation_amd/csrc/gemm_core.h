@@ -26,6 +26,7 @@ static inline FastDiv make_fastdiv(uint32_t d) {
 
 struct GemmParams {
   int M, N, K, batch, split, ktile_per_split;
+  int chunks_per_split;  // 32-deep K chunks per split piece (host-side planning)
   const float* A; int64_t lda, a_bs;
   const float* B; int64_t ldb, b_bs;
   float* C; int64_t ldc, c_bs;
@@ -321,15 +322,22 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int 
 // tile (tm, tn) for a linear workgroup id over tiles_m x tiles_n tiles: XCD-aware
 // remap (blocks b, b+8, ... share an XCD), then grouped raster so concurrently running
 // tiles of one XCD reuse A row-panels (group_m rows of tiles) and B column-panels.
-__device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles, int tiles_m, int& tm, int& tn) {
+// XCD-aware linear order: workgroup ids b, b+8, ... (one XCD) take one contiguous range
+// of [0, n), so neighbouring jobs share that XCD's L2.
+__device__ __forceinline__ int xcd_lin(int bid, int n) {
+  const int q = n / 8, r = n % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int ntiles, int tiles_m, int& tm, int& tn,
+                                        bool remap = true) {
   if (p.group_m <= 0) {  // plain raster: n fastest
     tm = bid / p.tiles_n;
     tn = bid % p.tiles_n;
     return;
   }
-  const int q = ntiles / 8, r = ntiles % 8;
-  const int xcd = bid % 8, idx = bid / 8;
-  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  const int lin = remap ? xcd_lin(bid, ntiles) : bid;
   const int per_group = p.group_m * p.tiles_n;
   const int grp = lin / per_group;
   const int first_m = grp * p.group_m;
@@ -356,12 +364,17 @@ __device__ __forceinline__ GemmJob job_of(const GemmParams& p) {
   }
   bid -= n1;
   const int n2 = p.tiles_m * p.tiles_n;
+  // The XCD remap runs over all (batch entry, K piece, tile) jobs, piece-major: every tile
+  // of one K piece (and of one batch entry) lands on one XCD, so a piece's operand rows --
+  // e.g. the NHWC pixels the im2col columns of a weight-gradient GEMM gather once per
+  // tap -- are fetched into one L2 instead of up to eight.
+  if (p.group_m > 0) bid = xcd_lin(bid, n2 * p.batch * p.split);
   const int zb = bid / n2, t2 = bid - zb * n2;
   j.b = zb / p.split;
   j.sidx = zb - j.b * p.split;
   j.split = p.split > 1;
   int tm2;
-  tile_of(p, t2, n2, p.tiles_m, tm2, j.tn);
+  tile_of(p, t2, n2, p.tiles_m, tm2, j.tn, false);
   j.tm = p.tiles_m1 + tm2;
   j.cid = j.b * n2 + tm2 * p.tiles_n + j.tn;
   return j;

@@ -99,6 +99,7 @@ struct WinParams {
   float* dq; float* dk; int64_t dqk_ld;
   float* dv; int64_t dv_ld;
   float* partial;  // [nwin][heads][T + 2*HD]: bias-table gradient, pad-key k / v gradient sums
+  int off32;       // every row * ld of the backward's column operands fits a 24x24 -> 32-bit multiply
 };
 
 // ---------------------------------------------------------------------------
@@ -334,11 +335,74 @@ __device__ __forceinline__ float col_val(const float* base, int64_t ld, const fl
 // compile-time relative-position-table column of key token `key`
 __host__ __device__ constexpr int key_tab(int key) { return (key / 7) * 13 + key % 7; }
 
+// Fast path of a window with no pad tokens (all 49 tokens are real rows, tokens >= 49 are MFMA
+// padding): which window tokens ti*32 + acc_row(r, h) / 2j + h are real is known at compile
+// time except for one register / pair, where it depends on the lane half.
+//   kind 0: real in both halves, 1: real only in half 0, 2: padding in both
+__host__ __device__ constexpr int acc_tok_kind(int ti, int r) {
+  return (ti * 32 + (r & 3) + 8 * (r >> 2) + 4 >= WA_N) ? ((ti * 32 + (r & 3) + 8 * (r >> 2) >= WA_N) ? 2 : 1) : 0;
+}
+__host__ __device__ constexpr int pair_tok_kind(int j) { return 2 * j + 1 >= WA_N ? (2 * j >= WA_N ? 2 : 1) : 0; }
+
+// Per-lane column values c[j] = scale * X[token 2j + h][col0 + l31] (j < 25).  FAST: every
+// token < 49 is a real row (no pad tokens in the window) and row * ld fits 32 bits, so the
+// address is one 24-bit multiply-add from the row table; token 49 (j = 24, half 1) is padding.
+template <bool FAST>
+__device__ __forceinline__ void fetch_pairs(float (&c)[25], const float* base, int64_t ld, const float* pad,
+                                            const int* rt, int col0, int l31, int h, float scale) {
+#ifdef WA_STUDY_NO_COLS
+  for (int j = 0; j < 25; ++j) c[j] = scale * (float)(j + l31);
+  return;
+#endif
+  if (FAST) {
+    const float* cb = base + col0 + l31;
+#pragma unroll
+    for (int j = 0; j < 25; ++j) {
+      const int kind = pair_tok_kind(j);
+      const float v = cb[__umul24((unsigned)rt[kind ? 2 * j : 2 * j + h], (unsigned)ld)];
+      c[j] = (kind && h) ? 0.f : scale * v;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 25; ++j) c[j] = scale * col_val(base, ld, pad, rt[2 * j + h], col0 + l31);
+  }
+}
+
+// c[t][r] = X[token t*32 + acc_row(r, h)][col0 + l31], the key rows of the accumulator layout
+template <bool FAST>
+__device__ __forceinline__ void fetch_keys(float (&c)[2][16], const float* base, int64_t ld, const float* pad,
+                                           const int* rt, int col0, int l31, int h) {
+#ifdef WA_STUDY_NO_COLS
+  for (int t = 0; t < 2; ++t)
+    for (int r = 0; r < 16; ++r) c[t][r] = (float)(r + t + l31);
+  return;
+#endif
+  if (FAST) {
+    const float* cb = base + col0 + l31;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kind = acc_tok_kind(t, r);
+        if (kind == 2) {
+          c[t][r] = 0.f;
+          continue;
+        }
+        const float v = cb[__umul24((unsigned)rt[kind ? t * 32 + acc_row(r, 0) : t * 32 + acc_row(r, h)], (unsigned)ld)];
+        c[t][r] = (kind && h) ? 0.f : v;
+      }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) c[t][r] = col_val(base, ld, pad, rt[t * 32 + acc_row(r, h)], col0 + l31);
+  }
+}
+
 template <int WS, int HD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void winattn_bwd_kernel(
     WinParams p, const float* __restrict__ biasT, int nitems) {
   __shared__ float tbuf[WA_WAVES][WA_NP][WA_TP];
-  __shared__ float tabg[WA_WAVES][WA_T + 3];
   __shared__ float padk[WA_WAVES][WA_HD], padv[WA_WAVES][WA_HD];
   __shared__ int8_t regs[WA_WAVES][WA_NP];
   __shared__ int rowtab[WA_WAVES][WA_NP];
@@ -347,10 +411,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const WaItem it = wa_item(p, nitems);
   const Win<WS> w(g, it.win);
   const int col0 = it.hh * HD;
-  for (int e = lane; e < WA_T + 3; e += 64) tabg[wv][e] = 0.f;
-  rowtab[wv][lane] = lane < WA_N ? w.row(g, lane) : -2;
+  // the saved log-sum-exp of this lane's two query columns, first: the softmax gradient waits on it
+  float lse[2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const int q = n * 32 + l31;
+    lse[n] = (q < WA_N) ? p.lse[(int64_t)it.item * WA_N + q] : INFINITY;  // +inf: P = 0
+  }
+  const int myrow = lane < WA_N ? w.row(g, lane) : -2;
+  rowtab[wv][lane] = myrow;
   if (lane < HD) { padk[wv][lane] = 0.f; padv[wv][lane] = 0.f; }
   const bool border = wa_regions(p, w, regs[wv], lane);
+  // wave-uniform: a window without pad tokens (most of them) takes the predicate-free fast path
+#ifdef WA_STUDY_NO_FAST
+  const bool fast = false;
+#else
+  const bool fast = p.off32 && __ballot(myrow == -1) == 0;
+#endif
 
   wa_f16x s[2][2], dp[2][2];  // S^T / P^T and dP^T / dS^T  [key tile][query tile]
   load_bias(s, biasT + (size_t)it.hh * 4096, lane);
@@ -392,43 +469,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int r = 0; r < 16; ++r) dp[a][b][r] = 0.f;
     mma_hd(dp, vf, df);  // dP^T[key][q] = sum_d V[key][d] dO[q][d]
   }
-  wave_lds_sync();  // tabg, pads, regs, rowtab
+  wave_lds_sync();  // pads, regs, rowtab
   // Column operands of the three products over the score tiles are fetched one phase
   // ahead (each is a burst of per-lane L2 loads): dO columns now, land under the
   // softmax-gradient pass; K columns before dV's MFMAs; Q columns before dQ's.
   float dc[25];
-#pragma unroll
-  for (int j = 0; j < 25; ++j) dc[j] = col_val(p.dout, p.out_ld, nullptr, rowtab[wv][2 * j + h], col0 + l31);
-  {
-    float lse[2];
-    int bq[2];
+  if (fast) fetch_pairs<true>(dc, p.dout, p.out_ld, nullptr, rowtab[wv], col0, l31, h, 1.f);
+  else fetch_pairs<false>(dc, p.dout, p.out_ld, nullptr, rowtab[wv], col0, l31, h, 1.f);
+  if (border) {  // shift mask (-100 across regions): last window row / column only
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-      const int q = n * 32 + l31;
-      lse[n] = (q < WA_N) ? p.lse[(int64_t)it.item * WA_N + q] : INFINITY;  // +inf: P = 0
-      bq[n] = q < WA_N ? (q / WS + WS - 1) * (2 * WS - 1) + q % WS + WS - 1 : -1;
-    }
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int rq = border ? regs[wv][n * 32 + l31] : 0;
+      const int rq = regs[wv][n * 32 + l31];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key0 = t * 32 + acc_row(r, 0);  // key of lane half 0; half 1: key0 + 4
-          const int key = key0 + 4 * h;
-          float sv = s[t][n][r];
-          if (border && regs[wv][key] != rq) sv -= 100.f;
-          const float pr = __expf(sv - lse[n]);
-          const float ds = pr * (dp[t][n][r] - D[n]);
-          s[t][n][r] = pr;
-          dp[t][n][r] = ds;
-          const bool kin = h ? (key0 + 4 < WA_N) : (key0 < WA_N);
-          const int kt = h ? key_tab(key0 + 4) : key_tab(key0);
-          if (bq[n] >= 0 && kin) atomicAdd(&tabg[wv][bq[n] - kt], ds);
-        }
+        for (int r = 0; r < 16; ++r)
+          if (regs[wv][t * 32 + acc_row(r, h)] != rq) s[t][n][r] -= 100.f;
     }
   }
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pr = __expf(s[t][n][r] - lse[n]);
+        dp[t][n][r] = pr * (dp[t][n][r] - D[n]);  // dS^T
+        s[t][n][r] = pr;                          // P^T
+      }
   // ---- products over the score tiles, each read back from the per-wave LDS image ----
   auto to_lds = [&](const wa_f16x (&x)[2][2]) {
 #pragma unroll
@@ -450,6 +518,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti) acc[ti] = mfma32(tbuf[wv][ti * 32 + l31][2 * j + h], colv[j], acc[ti]);
     if (!it.active) return;
+#ifdef WA_STUDY_NO_STORE
+    if (acc[0][0] == 1.2345f && acc[1][3] == 2.5f) gbase[l31] = acc[1][1];
+    return;
+#endif
+    if (fast) {
+      float* gb = gbase + col0 + l31;
+      const int* rt = rowtab[wv];
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kind = acc_tok_kind(ti, r);
+          if (kind == 2 || (kind == 1 && h)) continue;
+          gb[__umul24((unsigned)rt[ti * 32 + acc_row(r, h)], (unsigned)gld)] = acc[ti][r];
+        }
+      return;
+    }
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -464,18 +549,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   {
     to_lds(s);
     wave_lds_sync();
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) kc[t][r] = col_val(p.k, p.qk_ld, p.k_pad, rowtab[wv][t * 32 + acc_row(r, h)], col0 + l31);
+    if (fast) fetch_keys<true>(kc, p.k, p.qk_ld, p.k_pad, rowtab[wv], col0, l31, h);
+    else fetch_keys<false>(kc, p.k, p.qk_ld, p.k_pad, rowtab[wv], col0, l31, h);
     key_side(dc, p.dv, p.dv_ld, padv[wv]);
   }
   wave_lds_sync();  // every P^T read done
   to_lds(dp);
   wave_lds_sync();
   float qc[25];
-#pragma unroll
-  for (int j = 0; j < 25; ++j) qc[j] = p.scale * col_val(p.q, p.qk_ld, p.q_pad, rowtab[wv][2 * j + h], col0 + l31);
+  if (fast) fetch_pairs<true>(qc, p.q, p.qk_ld, p.q_pad, rowtab[wv], col0, l31, h, p.scale);
+  else fetch_pairs<false>(qc, p.q, p.qk_ld, p.q_pad, rowtab[wv], col0, l31, h, p.scale);
   // dQ^T[d][q] = sum_key K[key][d] dS^T[key][q]  (K columns from global, dS^T from LDS)
   {
     wa_f16x dq[2];
@@ -505,10 +588,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
   // dK[key][d] = sum_q dS^T[key][q] (scale Q)[q][d]
   key_side(qc, p.dk, p.dqk_ld, padk[wv]);
-  wave_lds_sync();  // tabg, pads complete
+  // Relative-position-bias gradient from the dS^T image still in LDS, deterministic and
+  // without atomics: with key (ky, kx), query (qy, qx), table slot (qy-ky+6)*13 + (qx-kx+6).
+  // Stage 1: lane (ky, qy) sums the 13 diagonals of its 7x7 block, E[ky][qy][dx] =
+  //   sum_kx dS^T[(ky,kx)][(qy,kx+dx)] (compile-time LDS offsets and register indices).
+  // Stage 2: slot (dy, dx) = sum_ky E[ky][ky+dy][dx], E staged through the same LDS image.
+  float E[13];
+#pragma unroll
+  for (int e = 0; e < 13; ++e) E[e] = 0.f;
+  const int sky = lane / WS, sqy = lane - sky * WS;
+  if (lane < WA_N) {
+    const float* blk = &tbuf[wv][sky * WS][sqy * WS];
+#pragma unroll
+    for (int kx = 0; kx < WS; ++kx)
+#pragma unroll
+      for (int qx = 0; qx < WS; ++qx) E[qx - kx + WS - 1] += blk[kx * WA_TP + qx];
+  }
+  wave_lds_sync();  // every read of the dS^T image done
+  constexpr int ND = 2 * WS - 1;
+  float* Eb = &tbuf[wv][0][0];  // [ky][qy][dx]
+  if (lane < WA_N) {
+#pragma unroll
+    for (int e = 0; e < ND; ++e) Eb[lane * ND + e] = E[e];
+  }
+  wave_lds_sync();  // E, pads complete
   if (it.active) {
     float* P = p.partial + (int64_t)it.item * (WA_T + 2 * HD);
-    for (int e = lane; e < WA_T; e += 64) P[e] = tabg[wv][e];
+    for (int e = lane; e < WA_T; e += 64) {
+      const int dy = e / ND - (WS - 1), dxi = e % ND;
+      const int ky0 = max(0, -dy), ky1 = min(WS - 1, WS - 1 - dy);
+      float acc = 0.f;
+      for (int ky = ky0; ky <= ky1; ++ky) acc += Eb[(ky * WS + ky + dy) * ND + dxi];
+      P[e] = acc;
+    }
     if (lane < HD) {
       P[WA_T + lane] = padk[wv][lane];
       P[WA_T + HD + lane] = padv[wv][lane];
@@ -574,6 +686,13 @@ static int make_params(const mdemi_winattn_desc* d, WinParams& p, int& nwin) {
   p.lse = d->lse;
   p.dout = d->dout; p.dq = d->dq; p.dk = d->dk; p.dqk_ld = d->dqk_ld; p.dv = d->dv; p.dv_ld = d->dv_ld;
   p.partial = (float*)d->workspace;
+  {
+    const int64_t rows = (int64_t)d->B * d->H * d->W;
+    const int64_t lds[4] = {d->qk_ld, d->out_ld, d->dqk_ld, d->dv_ld};
+    bool ok = rows < (1 << 24);
+    for (int64_t ld : lds) ok = ok && ld >= 0 && ld < (1 << 24) && rows * ld < (int64_t(1) << 32);
+    p.off32 = ok;
+  }
   nwin = d->B * p.g.nWh * p.g.nWw;
   return MDEMI_OK;
 }
