@@ -26,7 +26,6 @@ static inline FastDiv make_fastdiv(uint32_t d) {
 
 struct GemmParams {
   int M, N, K, batch, split, ktile_per_split;
-  int chunks_per_split;  // 32-deep K chunks per split piece (host-side planning)
   const float* A; int64_t lda, a_bs;
   const float* B; int64_t ldb, b_bs;
   float* C; int64_t ldc, c_bs;

@@ -89,15 +89,15 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const fl
 //   2: as 0 capped at 128 VGPRs (4 waves/SIMD; spills)
 //   3: BK32, 2 buffers (2 workgroups/CU by LDS)   4: BK32, 1 buffer   5: as 3, [row][k]
 //   6: 256-row tile (waves of 128x64), BK32, 1 buffer   7: 256-row tile, BK16, 2 buffers
-//   8: BK64, 1 buffer (half the barriers per MFMA of 4; only where every split-K piece is
-//      a whole number of 64-deep tiles)
+//   (a BK64 single-buffer variant measured no faster than 4 on the model's shapes:
+//   profiles/round3/gemm_study_bk64.txt)
 // No variant wins every shape (e.g. weight-gradient GEMMs over few output
 // tiles want BK32/2 buffers, token-major forwards want BK32/1 buffer), so by
 // default each distinct (layouts, ops, M, N, K, batch, split) is timed once
 // over the candidates on first use and the winner cached.  All variants add
 // the k products in the same order and split K at the same 32-element
 // boundaries, so the choice never changes a result bit.
-constexpr int NVARIANTS = 9;
+constexpr int NVARIANTS = 8;
 static int g_variant = -1;  // -1: autotune per shape
 // A/B switches (environment, read once): MDEMI_GEMM_TAIL_SPLIT=0 disables the tail split,
 // MDEMI_GEMM_INLINE_REDUCE=0 combines split-K slabs with the separate reduce kernel.
@@ -122,9 +122,7 @@ static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
   return f32_pick_part3(al, bl, aop, bop, v);
 }
 
-static int variant_bk(int v, int mode) {
-  return mode != GEMM_F32 ? 32 : (v == 8 ? 64 : ((v >= 3 && v != 7) ? 32 : 16));
-}
+static int variant_bk(int v, int mode) { return mode != GEMM_F32 ? 32 : ((v >= 3 && v != 7) ? 32 : 16); }
 static int variant_rows(int v, int mode) { return (mode != GEMM_F32 ? v == 2 : (v == 6 || v == 7)) ? 2 * GBM : GBM; }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -237,10 +235,8 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
   const int want = tp.split > 1 ? tp.split : d->split_k;
   const int split = want < kc ? want : kc;
   const int chunks_per_split = (int)cdiv(kc, split);
-  // BK 64: two chunks per K tile (launch() rejects an odd split piece for that variant)
-  p.ktile_per_split = GBK > CH ? chunks_per_split / (GBK / CH) : chunks_per_split * (CH / GBK);
+  p.ktile_per_split = chunks_per_split * (CH / GBK);
   p.split = (int)cdiv(kc, chunks_per_split);
-  p.chunks_per_split = chunks_per_split;
   p.m_split = (tp.split > 1 && p.split > 1) ? tp.m_split : 0;
   p.tile_cnt = nullptr;
   // vector loads need every row start 16-B aligned and whole quads in range
@@ -318,10 +314,6 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mod
   }
   GemmParams p;
   fill_params(d, p, variant, mode);
-  if (p.split > 1 && p.ktile_per_split * variant_bk(variant, mode) != p.chunks_per_split * 32) {
-    set_error("gemm: variant %d needs split-K pieces of whole %d-deep tiles", variant, variant_bk(variant, mode));
-    return MDEMI_EUNSUP;
-  }
   float* rowsum_part = nullptr;
   if (p.split > 1) {
     const size_t need = slab_bytes(d, p) + rowsum_bytes(d, p) + colsum_combine_bytes(d, p);
@@ -390,10 +382,10 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
     if (it != g_tuned.end()) return it->second;
   }
   if (!tunable(d, st)) return 0;
-  static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7, 8};
+  static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7};
   static const int cands_m16[] = {0, 1, 2};
   const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
-  const int ncand = mode != GEMM_F32 ? 3 : 8;
+  const int ncand = mode != GEMM_F32 ? 3 : 7;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 0;
   int best = 0;

@@ -26,7 +26,7 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   constexpr int WTM = BMT / 2;   // wave tile rows
   constexpr int FAT = NA * FA;   // floats of the A images
   static_assert(NBUF == 2 || NBUF == 1, "NBUF");
-  static_assert(BK == 16 || BK == 32 || BK == 64, "BK");
+  static_assert(BK == 16 || BK == 32, "BK");
   static_assert(BMT == 128 || BMT == 256, "BMT");
   __shared__ __attribute__((aligned(16))) float smem[NBUF * (FAT + FB)];
 
@@ -189,7 +189,6 @@ static KernelFn pick_variant(int v) {
     case 5: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 2, true, false, 2>;
     case 6: return gemm_f32_kernel<AL, BL, AOP, BOP, 32, 1, true, true, 2, 256>;
     case 7: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 2, 256>;
-    case 8: return gemm_f32_kernel<AL, BL, AOP, BOP, 64, 1, true, true, 2>;
     default: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 2>;
   }
 }

@@ -322,7 +322,14 @@ __global__ __launch_bounds__(256) void winattn_fwd_kernel(WinParams p, const flo
 // Q[q][l31], dO[q][l31]) come straight from global rows (L2 hits).  The
 // relative-position-bias gradient is gathered through per-wave LDS atomics;
 // pad keys (whose k / v were the Linear bias) fold into per-item sums.
-constexpr int WA_TP = WA_NP + 1;
+#ifdef WA_OCC3  // measured alternative (tools/wa_study.sh wa_occ3 -DWA_OCC3): 2.6 % slower per NYU step
+// score image of 56 key rows (keys >= 56 are padding: never stored, only read as discarded
+// MFMA rows) and pitch 57 (>= the 50 query columns the products read; odd: conflict-free
+// column reads): 53 KB per workgroup -> 3 workgroups per CU
+constexpr int WA_TR = 56, WA_TP = 57;
+#else
+constexpr int WA_TR = WA_NP, WA_TP = WA_NP + 1;
+#endif
 
 // Column fetch for a window token through the wave's row table (rowtab[tok] =
 // the token's row, -1 for a pad token, -2 for MFMA padding): value of column
@@ -350,10 +357,6 @@ __host__ __device__ constexpr int pair_tok_kind(int j) { return 2 * j + 1 >= WA_
 template <bool FAST>
 __device__ __forceinline__ void fetch_pairs(float (&c)[25], const float* base, int64_t ld, const float* pad,
                                             const int* rt, int col0, int l31, int h, float scale) {
-#ifdef WA_STUDY_NO_COLS
-  for (int j = 0; j < 25; ++j) c[j] = scale * (float)(j + l31);
-  return;
-#endif
   if (FAST) {
     const float* cb = base + col0 + l31;
 #pragma unroll
@@ -372,11 +375,6 @@ __device__ __forceinline__ void fetch_pairs(float (&c)[25], const float* base, i
 template <bool FAST>
 __device__ __forceinline__ void fetch_keys(float (&c)[2][16], const float* base, int64_t ld, const float* pad,
                                            const int* rt, int col0, int l31, int h) {
-#ifdef WA_STUDY_NO_COLS
-  for (int t = 0; t < 2; ++t)
-    for (int r = 0; r < 16; ++r) c[t][r] = (float)(r + t + l31);
-  return;
-#endif
   if (FAST) {
     const float* cb = base + col0 + l31;
 #pragma unroll
@@ -400,9 +398,14 @@ __device__ __forceinline__ void fetch_keys(float (&c)[2][16], const float* base,
 }
 
 template <int WS, int HD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void winattn_bwd_kernel(
+#ifdef WA_OCC3
+#define WA_BWD_OCC 3
+#else
+#define WA_BWD_OCC 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WA_BWD_OCC, WA_BWD_OCC))) void winattn_bwd_kernel(
     WinParams p, const float* __restrict__ biasT, int nitems) {
-  __shared__ float tbuf[WA_WAVES][WA_NP][WA_TP];
+  __shared__ float tbuf[WA_WAVES][WA_TR][WA_TP];
   __shared__ float padk[WA_WAVES][WA_HD], padv[WA_WAVES][WA_HD];
   __shared__ int8_t regs[WA_WAVES][WA_NP];
   __shared__ int rowtab[WA_WAVES][WA_NP];
@@ -423,17 +426,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (lane < HD) { padk[wv][lane] = 0.f; padv[wv][lane] = 0.f; }
   const bool border = wa_regions(p, w, regs[wv], lane);
   // wave-uniform: a window without pad tokens (most of them) takes the predicate-free fast path
-#ifdef WA_STUDY_NO_FAST
-  const bool fast = false;
-#else
   const bool fast = p.off32 && __ballot(myrow == -1) == 0;
-#endif
 
   wa_f16x s[2][2], dp[2][2];  // S^T / P^T and dP^T / dS^T  [key tile][query tile]
   load_bias(s, biasT + (size_t)it.hh * 4096, lane);
   int trow[2];
   bool treal[2];
-  float D[2];
   {
     float4 kf[2][4], qf[2][4];
 #pragma unroll
@@ -446,6 +444,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     mma_hd(s, kf, qf);  // S^T[key][q]
   }
+  wave_lds_sync();  // pads, regs, rowtab
+  if (border) {  // shift mask (-100 across regions): last window row / column only
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int rq = regs[wv][n * 32 + l31];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (regs[wv][t * 32 + acc_row(r, h)] != rq) s[t][n][r] -= 100.f;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[t][n][r] = __expf(s[t][n][r] - lse[n]);  // P^T
+  // ---- products over the score tiles, each read back from the per-wave LDS image ----
+  auto to_lds = [&](const wa_f16x (&x)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+#ifdef WA_OCC3
+          if (t * 32 + acc_row(r, 0) >= WA_TR || (n == 1 && l31 >= WA_TP - 32)) continue;
+#endif
+          tbuf[wv][t * 32 + acc_row(r, h)][n * 32 + l31] = x[t][n][r];
+        }
+  };
+  // acc[ti][r] = sum_q tbuf[ti*32 + l31][q] * col[q], q = 2j + h; row key = ti*32 + acc_row(r, h), column d = l31
+  auto key_side = [&](const float (&colv)[25], float* gbase, int64_t gld, float* padacc) {
+    wa_f16x acc[2];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ti][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 25; ++j)
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) acc[ti] = mfma32(tbuf[wv][ti * 32 + l31][2 * j + h], colv[j], acc[ti]);
+    if (!it.active) return;
+    if (fast) {
+      float* gb = gbase + col0 + l31;
+      const int* rt = rowtab[wv];
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kind = acc_tok_kind(ti, r);
+          if (kind == 2 || (kind == 1 && h)) continue;
+          gb[__umul24((unsigned)rt[ti * 32 + acc_row(r, h)], (unsigned)gld)] = acc[ti][r];
+        }
+      return;
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rowtab[wv][ti * 32 + acc_row(r, h)];
+        if (row >= 0) gbase[(int64_t)row * gld + col0 + l31] = acc[ti][r];
+        else if (row == -1) atomicAdd(&padacc[l31], acc[ti][r]);  // pad key: into the Linear-bias gradient
+      }
+  };
+  // dV[key][d] = sum_q P^T[key][q] dO[q][d]; P^T leaves the registers here and is read back
+  // from LDS for dS, so P^T and dP^T are never live together
+  {
+    to_lds(s);
+    wave_lds_sync();
+    float dc[25];
+    if (fast) fetch_pairs<true>(dc, p.dout, p.out_ld, nullptr, rowtab[wv], col0, l31, h, 1.f);
+    else fetch_pairs<false>(dc, p.dout, p.out_ld, nullptr, rowtab[wv], col0, l31, h, 1.f);
+    key_side(dc, p.dv, p.dv_ld, padv[wv]);
+  }
+  float D[2];
   {
     float4 vf[2][4], df[2][4];
 #pragma unroll
@@ -469,90 +544,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int r = 0; r < 16; ++r) dp[a][b][r] = 0.f;
     mma_hd(dp, vf, df);  // dP^T[key][q] = sum_d V[key][d] dO[q][d]
   }
-  wave_lds_sync();  // pads, regs, rowtab
-  // Column operands of the three products over the score tiles are fetched one phase
-  // ahead (each is a burst of per-lane L2 loads): dO columns now, land under the
-  // softmax-gradient pass; K columns before dV's MFMAs; Q columns before dQ's.
-  float dc[25];
-  if (fast) fetch_pairs<true>(dc, p.dout, p.out_ld, nullptr, rowtab[wv], col0, l31, h, 1.f);
-  else fetch_pairs<false>(dc, p.dout, p.out_ld, nullptr, rowtab[wv], col0, l31, h, 1.f);
-  if (border) {  // shift mask (-100 across regions): last window row / column only
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int rq = regs[wv][n * 32 + l31];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (regs[wv][t * 32 + acc_row(r, h)] != rq) s[t][n][r] -= 100.f;
-    }
-  }
+  // dS^T = P^T (dP^T - D), P^T read back from the LDS image (0 where the image has no slot:
+  // padding keys / queries)
 #pragma unroll
   for (int n = 0; n < 2; ++n)
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pr = __expf(s[t][n][r] - lse[n]);
-        dp[t][n][r] = pr * (dp[t][n][r] - D[n]);  // dS^T
-        s[t][n][r] = pr;                          // P^T
-      }
-  // ---- products over the score tiles, each read back from the per-wave LDS image ----
-  auto to_lds = [&](const wa_f16x (&x)[2][2]) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) tbuf[wv][t * 32 + acc_row(r, h)][n * 32 + l31] = x[t][n][r];
-  };
-  // acc[ti][r] = sum_q tbuf[ti*32 + l31][q] * col[q], q = 2j + h; row key = ti*32 + acc_row(r, h), column d = l31
-  auto key_side = [&](const float (&colv)[25], float* gbase, int64_t gld, float* padacc) {
-    wa_f16x acc[2];
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[ti][r] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 25; ++j)
-#pragma unroll
-      for (int ti = 0; ti < 2; ++ti) acc[ti] = mfma32(tbuf[wv][ti * 32 + l31][2 * j + h], colv[j], acc[ti]);
-    if (!it.active) return;
-#ifdef WA_STUDY_NO_STORE
-    if (acc[0][0] == 1.2345f && acc[1][3] == 2.5f) gbase[l31] = acc[1][1];
-    return;
+        float pr;
+#ifdef WA_OCC3
+        if (t * 32 + acc_row(r, 0) >= WA_TR) pr = 0.f;
+        else if (n == 1) pr = l31 < WA_TP - 32 ? tbuf[wv][t * 32 + acc_row(r, h)][32 + min(l31, WA_TP - 33)] : 0.f;
+        else
 #endif
-    if (fast) {
-      float* gb = gbase + col0 + l31;
-      const int* rt = rowtab[wv];
-#pragma unroll
-      for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kind = acc_tok_kind(ti, r);
-          if (kind == 2 || (kind == 1 && h)) continue;
-          gb[__umul24((unsigned)rt[ti * 32 + acc_row(r, h)], (unsigned)gld)] = acc[ti][r];
-        }
-      return;
-    }
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rowtab[wv][ti * 32 + acc_row(r, h)];
-        if (row >= 0) gbase[(int64_t)row * gld + col0 + l31] = acc[ti][r];
-        else if (row == -1) atomicAdd(&padacc[l31], acc[ti][r]);  // pad key: into the Linear-bias gradient
+        pr = tbuf[wv][t * 32 + acc_row(r, h)][n * 32 + l31];
+        dp[t][n][r] = pr * (dp[t][n][r] - D[n]);
       }
-  };
-  // dV[key][d] = sum_q P^T[key][q] dO[q][d]
   float kc[2][16];
-  {
-    to_lds(s);
-    wave_lds_sync();
-    if (fast) fetch_keys<true>(kc, p.k, p.qk_ld, p.k_pad, rowtab[wv], col0, l31, h);
-    else fetch_keys<false>(kc, p.k, p.qk_ld, p.k_pad, rowtab[wv], col0, l31, h);
-    key_side(dc, p.dv, p.dv_ld, padv[wv]);
-  }
+  if (fast) fetch_keys<true>(kc, p.k, p.qk_ld, p.k_pad, rowtab[wv], col0, l31, h);
+  else fetch_keys<false>(kc, p.k, p.qk_ld, p.k_pad, rowtab[wv], col0, l31, h);
   wave_lds_sync();  // every P^T read done
   to_lds(dp);
   wave_lds_sync();
