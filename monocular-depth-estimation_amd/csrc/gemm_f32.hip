@@ -91,13 +91,16 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const fl
 //   6: 256-row tile (waves of 128x64), BK32, 1 buffer   7: 256-row tile, BK16, 2 buffers
 //   (a BK64 single-buffer variant measured no faster than 4 on the model's shapes:
 //   profiles/round3/gemm_study_bk64.txt)
+//   8..11: direct-to-LDS staging (buffer_load ... lds, gemm_glds_kernel.h), dense 16-B
+//   operands without a load-time op only: 8 128-row BK32, 9 256-row BK16, 10 256-row
+//   BK32 (96 KiB, one workgroup per CU), 11 128-row BK16
 // No variant wins every shape (e.g. weight-gradient GEMMs over few output
 // tiles want BK32/2 buffers, token-major forwards want BK32/1 buffer), so by
 // default each distinct (layouts, ops, M, N, K, batch, split) is timed once
 // over the candidates on first use and the winner cached.  All variants add
 // the k products in the same order and split K at the same 32-element
 // boundaries, so the choice never changes a result bit.
-constexpr int NVARIANTS = 8;
+constexpr int NVARIANTS = 12;
 static int g_variant = -1;  // -1: autotune per shape
 // A/B switches (environment, read once): MDEMI_GEMM_TAIL_SPLIT=0 disables the tail split,
 // MDEMI_GEMM_INLINE_REDUCE=0 combines split-K slabs with the separate reduce kernel.
@@ -115,15 +118,35 @@ KernelFn f32_pick_part1(int al, int bl, int aop, int bop, int v);
 KernelFn f32_pick_part2(int al, int bl, int aop, int bop, int v);
 KernelFn f32_pick_part3(int al, int bl, int aop, int bop, int v);
 
+KernelFn glds_pick_part0(int al, int bl, int v);
+KernelFn glds_pick_part1(int al, int bl, int v);
+
 static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
+  if (v >= 8) {  // direct-to-LDS variants: dense operands without a load-time op
+    if (aop != MDEMI_OP_NONE || bop != MDEMI_OP_NONE) return nullptr;
+    if (KernelFn f = glds_pick_part0(al, bl, v)) return f;
+    return glds_pick_part1(al, bl, v);
+  }
   if (KernelFn f = f32_pick_part0(al, bl, aop, bop, v)) return f;
   if (KernelFn f = f32_pick_part1(al, bl, aop, bop, v)) return f;
   if (KernelFn f = f32_pick_part2(al, bl, aop, bop, v)) return f;
   return f32_pick_part3(al, bl, aop, bop, v);
 }
 
-static int variant_bk(int v, int mode) { return mode != GEMM_F32 ? 32 : ((v >= 3 && v != 7) ? 32 : 16); }
-static int variant_rows(int v, int mode) { return (mode != GEMM_F32 ? v == 2 : (v == 6 || v == 7)) ? 2 * GBM : GBM; }
+static int variant_bk(int v, int mode) {
+  if (mode != GEMM_F32) return 32;
+  if (v >= 8) return (v == 8 || v == 10) ? 32 : 16;
+  return (v >= 3 && v != 7) ? 32 : 16;
+}
+static int variant_rows(int v, int mode) {
+  return (mode != GEMM_F32 ? v == 2 : (v == 6 || v == 7 || v == 9 || v == 10)) ? 2 * GBM : GBM;
+}
+// the direct-to-LDS variants need dense operands that load as whole 16-B quads and no
+// load-time transform
+static bool glds_ok(const mdemi_gemm_desc* d, const GemmParams& p) {
+  return d->a_layout != MDEMI_L_CONV && d->b_layout != MDEMI_L_CONV && d->a_op == MDEMI_OP_NONE &&
+         d->b_op == MDEMI_OP_NONE && p.a_vec && p.b_vec;
+}
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -304,6 +327,11 @@ static size_t colsum_combine_bytes(const mdemi_gemm_desc* d, const GemmParams& p
 }
 
 static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mode) {
+  if (mode == GEMM_F32 && variant >= 8) {  // a forced direct-to-LDS variant on an operand it cannot stage
+    GemmParams q;
+    fill_params(d, q, variant, mode);
+    if (!glds_ok(d, q)) variant = 0;
+  }
   KernelFn fn = mode == GEMM_F32 ? pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant)
                                  : pick_kernel_m16(d->a_layout, d->b_layout, d->a_op, d->b_op,
                                                    mode == GEMM_BF16 ? 1 : 3, variant);
@@ -382,10 +410,15 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
     if (it != g_tuned.end()) return it->second;
   }
   if (!tunable(d, st)) return 0;
-  static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7};
+  static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11};
   static const int cands_m16[] = {0, 1, 2};
   const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
-  const int ncand = mode != GEMM_F32 ? 3 : 7;
+  int ncand = mode != GEMM_F32 ? 3 : 11;
+  if (mode == GEMM_F32) {
+    GemmParams q;
+    fill_params(d, q, 0, mode);
+    if (!glds_ok(d, q)) ncand = 7;
+  }
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 0;
   int best = 0;

@@ -15,6 +15,7 @@ using KernelFn = void (*)(GemmParams);
 //   PREF  register prefetch of the next tile before the MFMAs (issue early / write late)
 //   BMT   block-tile rows: 128 (2x2 waves of 64x64) or 256 (2x2 waves of 128x64, A staged as
 //         two 128-row images: twice the MFMAs per barrier and per B fragment)
+// Variants 8..11 stage by DMA straight into LDS (gemm_glds_kernel.h).
 template <int AL, int BL, int AOP, int BOP, int BK, int NBUF, bool PREF, bool TR, int OCC, int BMT = 128>
 __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void gemm_f32_kernel(GemmParams p) {
   using LA = Loader<AL, AOP, true, BK, TR>;
@@ -181,6 +182,7 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 
 template <int AL, int BL, int AOP, int BOP>
 static KernelFn pick_variant(int v) {
+  if (v >= 8) return nullptr;  // direct-to-LDS staging: gemm_glds_inst*.hip (gemm_f32.hip pick_kernel)
   switch (v) {
     case 1: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, false, 2>;
     case 2: return gemm_f32_kernel<AL, BL, AOP, BOP, 16, 2, true, true, 4>;

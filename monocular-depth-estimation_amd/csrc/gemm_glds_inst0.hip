@@ -1,0 +1,14 @@
+// Instantiations of the direct-to-LDS fp32 GEMM variants (gemm_glds_kernel.h), layout
+// pairs (KCONTIG, KCONTIG), (KCONTIG, MNCONTIG): their own translation units, so editing
+// the kernel rebuilds only these.
+#include "gemm_glds_kernel.h"
+
+namespace mdemi {
+
+void (*glds_pick_part0(int al, int bl, int v))(GemmParams) {
+  if (al == MDEMI_L_KCONTIG && bl == MDEMI_L_KCONTIG) return pick_glds<MDEMI_L_KCONTIG, MDEMI_L_KCONTIG>(v);
+  if (al == MDEMI_L_KCONTIG && bl == MDEMI_L_MNCONTIG) return pick_glds<MDEMI_L_KCONTIG, MDEMI_L_MNCONTIG>(v);
+  return nullptr;
+}
+
+}  // namespace mdemi

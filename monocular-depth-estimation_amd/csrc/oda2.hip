@@ -70,7 +70,12 @@ __global__ __launch_bounds__(256) void win_shuffle_kernel(const V* __restrict__ 
 constexpr int OS_MAXTAB = 511;  // 2 * num_emb - 1 with num_emb <= 256
 
 template <int T>
-__global__ __launch_bounds__(256) void ordered_softmax_fwd_kernel(const float* __restrict__ S, float* __restrict__ P,
+// S and P (forward) and dP and dS (backward) may alias: each row is read whole before it is
+// written, so neither pair is __restrict__.  Depth indices are clamped to [0, nemb-1] as they
+// are staged: the reference's floor(sigmoid(logit) * n - 1e-3) gives -1 where the sigmoid
+// underflows to 0 (logit < -88), and F.embedding raises there; the clamp keeps every table
+// and histogram access inside its LDS array instead of reading or adding out of bounds.
+__global__ __launch_bounds__(256) void ordered_softmax_fwd_kernel(const float* S, float* P,
                                                                   const int* __restrict__ idx,
                                                                   const float* __restrict__ table, int nwin,
                                                                   int heads, int nemb, float scale) {
@@ -82,7 +87,7 @@ __global__ __launch_bounds__(256) void ordered_softmax_fwd_kernel(const float* _
   for (int k = threadIdx.x; k < ntab; k += 256) tab[k] = table ? table[(int64_t)k * heads + h] : 0.f;
   for (int w = blockIdx.y; w < nwin; w += gridDim.y) {
     __syncthreads();
-    for (int t = threadIdx.x; t < T; t += 256) widx[t] = table ? idx[(int64_t)w * T + t] : 0;
+    for (int t = threadIdx.x; t < T; t += 256) widx[t] = table ? min(max(idx[(int64_t)w * T + t], 0), nemb - 1) : 0;
     __syncthreads();
     const int64_t base = ((int64_t)w * heads + h) * T * T;
     for (int row = wv; row < T; row += 4) {
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(256) void ordered_softmax_fwd_kernel(const float* _
 // relative index into part[blockIdx.y][k * heads + h] (the table's own layout)
 template <int T>
 __global__ __launch_bounds__(256) void ordered_softmax_bwd_kernel(const float* __restrict__ P,
-                                                                  const float* __restrict__ dP, float* __restrict__ dS,
+                                                                  const float* dP, float* dS,
                                                                   const int* __restrict__ idx, float* __restrict__ part,
                                                                   int nwin, int heads, int nemb, float scale) {
   constexpr int Q = T / 64;
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(256) void ordered_softmax_bwd_kernel(const float* _
   for (int w = blockIdx.y; w < nwin; w += gridDim.y) {
     __syncthreads();
     if (tab)
-      for (int t = threadIdx.x; t < T; t += 256) widx[t] = idx[(int64_t)w * T + t];
+      for (int t = threadIdx.x; t < T; t += 256) widx[t] = min(max(idx[(int64_t)w * T + t], 0), nemb - 1);
     __syncthreads();
     const int64_t base = ((int64_t)w * heads + h) * T * T;
     for (int row = wv; row < T; row += 4) {

@@ -267,8 +267,12 @@ def stream() -> int:
 _ws: dict = {}
 # Once a hipGraph has been captured, a workspace buffer superseded by a larger one
 # (a later eager call at a bigger shape) must never return to the allocator: the
-# graph keeps the raw addresses it was recorded with.  Before any capture,
-# superseded buffers are simply freed.
+# graph keeps the raw addresses it was recorded with.  Before any capture, a
+# superseded buffer is freed only after the device has drained: workspaces are
+# also used on side streams (GraphedPredictor's warm-up stream), and the caching
+# allocator would otherwise hand the block to a new allocation on its origin
+# stream while another stream's kernels still use it.  Growth happens in
+# warm-up only, so the synchronisation is rare.
 _ws_retired: list = []
 _graph_captured = False
 
@@ -293,8 +297,11 @@ def workspace(nbytes: int, device=None, slot: int = 0) -> torch.Tensor:
         if capturing:
             raise RuntimeError(f"mdemi: workspace slot {slot} must grow to {nbytes} bytes during hipGraph capture; "
                                "run the captured step eagerly first (warm-up) so every workspace is sized")
-        if buf is not None and _graph_captured:
-            _ws_retired.append(buf)
+        if buf is not None:
+            if _graph_captured:
+                _ws_retired.append(buf)
+            else:
+                torch.cuda.synchronize(device)
         buf = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=device)
         _ws[key] = buf
     return buf

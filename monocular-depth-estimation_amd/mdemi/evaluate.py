@@ -20,7 +20,6 @@ Every step is a libmdemi launch (flip: mdemi_flip_w / mdemi_flip_avg_w;
 resize: mdemi_bilinear_*; metrics: mdemi_depth_metrics); only the per-image
 metric rows (B x 10 fp64) come back to the host.
 """
-import time
 
 import torch
 
@@ -85,8 +84,8 @@ class GraphedPredictor:
                 predict_depth(model, self.static_in, self.flip_eval)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            time.sleep(0.5)  # let the process group's watchdog retire finished collectives (builder.Trainer)
+        from .train.builder import quiesce_process_group
+        quiesce_process_group()  # no eager collective may be polled by the watchdog mid-capture
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.static_out = predict_depth(model, self.static_in, self.flip_eval)

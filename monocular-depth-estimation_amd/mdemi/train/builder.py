@@ -38,8 +38,6 @@ from __future__ import annotations
 
 import math
 
-import time
-
 import torch
 import torch.nn as nn
 
@@ -87,12 +85,24 @@ def build_model(opt, drop_path=None):
     return model
 
 
+# loss.* keys of the in-scope reference configs; sog_weight names a loss term this framework
+# does not implement (0.0 in every in-scope config) and reduction_ratio configures only that
+# term -- a nonzero sog_weight is refused rather than silently dropped
+LOSS_KEYS = ("alpha", "beta", "per_image", "chamfer_weight", "si_weight", "sog_weight", "reduction_ratio")
+
+
 class TrainLoss:
     """SILog on the depth (+ chamfer_weight x the bin chamfer loss on AdaBins' edges /
     Depthformer's centres when loss.chamfer_weight > 0)."""
 
     def __init__(self, opt, model_name):
         lo = opt.get("loss", {})
+        unknown = sorted(set(lo) - set(LOSS_KEYS))
+        if unknown:
+            raise ValueError(f"loss keys {unknown} are not implemented by this framework (known: {LOSS_KEYS})")
+        if float(lo.get("sog_weight", 0.0)) != 0.0:
+            raise ValueError(f"loss.sog_weight={lo['sog_weight']}: the SOG loss term is not implemented "
+                             "(every in-scope reference config sets it to 0.0)")
         dmin, _ = _depth_range(opt)
         self.silog = SILogLoss(alpha=float(lo.get("alpha", 10.0)), beta=float(lo.get("beta", 0.15)),
                                per_image=bool(lo.get("per_image", False)), min_depth=dmin)
@@ -160,8 +170,27 @@ def freeze_bn(model):
             m.eval()
 
 
-# ProcessGroupNCCL's watchdog polls outstanding works every 100 ms (kWatchdogThreadSleepMillis)
-_WATCHDOG_RETIRE_S = 0.5
+def quiesce_process_group(works=()):
+    """Before a hipGraph capture on a process whose RCCL process group has run eager
+    collectives: wait for each eager Work, then block until ProcessGroupNCCL's watchdog
+    thread has retired every one of them (ProcessGroupNCCL::waitForPendingWorks returns
+    once the watchdog's work list and its completed-work list are both empty).  The
+    watchdog polls each listed work's HIP event (hipEventQuery); such a query issued
+    while this thread holds a global-mode capture is a capture-unsafe call from another
+    thread, which invalidates the capture and aborts the process.  Collectives issued
+    during the capture are never listed, so once the list is empty nothing else can
+    query mid-capture.  A no-op without an initialised process group; gloo groups have
+    no watchdog (nothing to wait for)."""
+    import torch.distributed as dist
+    for w in works:
+        w.wait()
+    torch.cuda.synchronize()
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    groups = [dist.distributed_c10d._get_default_group()]
+    for pg in groups:
+        if dist.get_backend(pg) == "nccl":
+            pg._wait_for_pending_works()
 
 
 class Trainer:
@@ -240,12 +269,9 @@ class Trainer:
             self._static = [(img.clone(), gt.clone()) for img, gt in batches]
             self._zero_grad(set_to_none=False)
             if self.ddp is not None:
-                # No collective of the eager steps may still be in flight, and the process
-                # group's watchdog thread must have retired them: it polls each outstanding
-                # work's HIP event, which a global-mode capture refuses (it aborts the
-                # process).  Captured collectives are never handed to the watchdog.
-                torch.cuda.synchronize()
-                time.sleep(_WATCHDOG_RETIRE_S)
+                # no eager collective may still be listed with the process group's watchdog
+                # when the global-mode capture begins (quiesce_process_group)
+                quiesce_process_group()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g), mf.matmul_precision(self.precision):
                 self._static_loss = self._body(self._static)
@@ -280,6 +306,27 @@ class Trainer:
             self.ddp.finish()
         self.optimizer.step()
         return total
+
+    def save(self, prefix, save_dir, current_iter, best_value, best_epoch=None, best_iter=None, model_only=False):
+        """common_utils.save_checkpoint of this trainer's model and optimizer at self.epoch."""
+        from ..utils.common_utils import save_checkpoint
+        save_checkpoint(prefix, self.model, self.optimizer, self.epoch, current_iter, best_value, save_dir,
+                        best_epoch=best_epoch, best_iter=best_iter, model_only=model_only)
+
+    def resume(self, path):
+        """Load a save_checkpoint file (the reference's format): model weights, optimizer
+        state (moments and per-parameter step counts), epoch, and the OneCycle position
+        = optimizer steps taken.  A captured step is re-captured after the next eager step
+        when the load replaced state tensors (FusedAdamW.layout_version).  Returns the file's
+        dict."""
+        from ..utils.common_utils import load_checkpoint
+        dev = next(self.model.parameters()).device
+        ck = load_checkpoint(path, self.model, self.optimizer, map_location=dev)
+        self.epoch = int(ck.get("epoch", 0) or 0)
+        if self.scheduler is not None:
+            self.scheduler.set_position(self.optimizer.step_count)
+        self.train_mode()
+        return ck
 
     def _zero_grad(self, set_to_none):
         if self.ddp is not None:

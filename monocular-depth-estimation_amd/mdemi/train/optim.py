@@ -314,6 +314,20 @@ class OneCycleLR:
             g["lr"], b1 = self.values(s, g)
             g["betas"] = (b1, g["betas"][1])
 
+    def state_dict(self):
+        return {"last_step": self.last_step, "total": self.total}
+
+    def load_state_dict(self, sd):
+        self.set_position(int(sd["last_step"]))
+
+    def set_position(self, s):
+        """Resume: the schedule after s scheduler steps (the optimizer steps a checkpoint
+        recorded), as if step() had been called s times since construction."""
+        if not 0 <= s <= self.total:
+            raise ValueError(f"OneCycleLR position {s} outside [0, {self.total}]")
+        self.last_step = s - 1
+        self.step()
+
     def hyper_table(self):
         """Row s = (lr, beta1, beta2, eps, weight_decay) per group after s scheduler steps,
         s = 0..total: FusedAdamW.set_schedule's rows for a captured train step (the optimizer

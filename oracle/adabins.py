@@ -6,6 +6,8 @@ torch.hub download in the reference (unet_adaptive_bins.py:129): parity unpinned
 import torch
 import torch.nn.functional as F
 
+from . import bnmode
+
 # Test hook (kink-aware comparisons): when set to a list of boolean tensors, every
 # ReLU / LeakyReLU of the head takes its branch from the next mask in call order
 # (mask = "pre-activation > 0" as the GPU forward decided it) instead of from the sign
@@ -25,7 +27,8 @@ def _kink_act(x, slope):
 
 
 def bn_train(P, pre, x, eps=1e-5):
-    return F.batch_norm(x, None, None, P[pre + "weight"], P[pre + "bias"], training=True, eps=eps)
+    """Batch statistics, or the running ones inside bnmode.eval_bn()."""
+    return bnmode.batch_norm(P, pre, x, eps)
 
 
 def upsample_bn(P, pre, x, concat_with):  # unet_adaptive_bins.py:8-24

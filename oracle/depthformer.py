@@ -8,6 +8,8 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import bnmode
+
 
 def ln(P, pre, x, eps=1e-5):
     return F.layer_norm(x, (x.shape[-1],), P[pre + "weight"], P[pre + "bias"], eps)
@@ -24,7 +26,7 @@ def conv_bn(P, pre, x, act=True, use_residual=True):  # layer_utils.py:6-34
     if k > 1:
         x = F.pad(x, (k // 2, k // 2, k // 2, k // 2), mode="replicate")
     x = F.conv2d(x, w)
-    x = F.batch_norm(x, None, None, P[pre + "bn.weight"], P[pre + "bn.bias"], training=True, eps=1e-5)
+    x = bnmode.batch_norm(P, pre + "bn.", x, 1e-5)
     if act:
         x = F.silu(x)
     if use_residual and w.shape[0] == w.shape[1]:

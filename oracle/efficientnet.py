@@ -17,6 +17,8 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import bnmode
+
 BN_EPS = 1e-3
 # (block type, repeats, kernel, stride, expansion, channels) of EfficientNet-B0, scaled below
 ARCH = [("ds", 1, 3, 1, 1, 16), ("ir", 2, 3, 2, 6, 24), ("ir", 2, 5, 2, 6, 40), ("ir", 3, 3, 2, 6, 80),
@@ -35,7 +37,7 @@ def conv_same(x, w, stride=1, groups=1, b=None):
 
 
 def bn(P, pre, x):
-    return F.batch_norm(x, None, None, P[pre + "weight"], P[pre + "bias"], training=True, eps=BN_EPS)
+    return bnmode.batch_norm(P, pre, x, BN_EPS)
 
 
 def se(P, pre, x):

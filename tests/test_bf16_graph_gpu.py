@@ -208,3 +208,64 @@ def test_graph_replays_draw_new_dropout_masks(mf):
     assert all(torch.isfinite(torch.tensor(losses)))
     # replays 3-5 see the same batch; dropout masks (and the weights) change between them
     assert len(set(losses[2:])) == 3
+
+
+def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
+    """BASELINE configs[4] at its own size: Depthformer v8 with the benchmark's decoder (hidden
+    256, 4 heads, 256 bins, 256 aux tokens) at NYU 480x640, batch 2, train mode, under bf16
+    matmuls, against the fp64 oracle (oracle.depthformer, pinned to the reference by
+    tests/golden/depthformer_v8.npz; restated B5 encoder): depth, centres, the 8 attention
+    maps and EVERY parameter gradient, each within the relative-L2 bounds above
+    (BF16_OUT_L2 outputs, BF16_GRAD_L2 gradients; vanishing gradients held against a floor of
+    1e-2 x the largest gradient norm, as in the golden case).  depthformer_v8.py:46-75,
+    decoder_v8.py:97-171."""
+    import numpy as np
+
+    import test_models_gpu as tm
+    from mdemi.model.Depthformer import DepthformerV8
+    from oracle import depthformer as odf
+    from oracle.weights import rng_array
+
+    torch.set_num_threads(16)
+    opt = {"hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256, "img_size": [480, 640],
+           "attn_drop_prob": 0.0, "drop_prob": 0.0}
+    m = DepthformerV8.build(opt, 1e-3, 10.0)
+    sd = tm._filled_state(m, 0.53, 0.03)
+    m = m.to(DEV).train()
+    img = torch.from_numpy(rng_array((2, 3, 480, 640), 84))
+    with mf.matmul_precision("bf16"):
+        depth, centers, attn = m(img.float().to(DEV))
+        dy = torch.from_numpy(rng_array(tuple(depth.shape), 85))
+        (depth * dy.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    P = {k: (v.detach().double().clone().requires_grad_(True) if torch.is_floating_point(v) else v)
+         for k, v in sd.items()}
+    dr, cr, ar = odf.depthformer_v8_full(P, img.double(), opt, 1e-3, 10.0)
+    (dr * dy.double()).sum().backward()
+
+    def rel_l2(a, r):
+        a, r = a.detach().double().cpu().reshape(-1), r.detach().double().reshape(-1)
+        return (torch.linalg.norm(a - r) / (torch.linalg.norm(r) + 1e-300)).item(), torch.linalg.norm(r).item()
+
+    outs = {"depth": rel_l2(depth, dr)[0], "centers": rel_l2(centers, cr)[0]}
+    for k, (a, r) in enumerate(zip(attn, ar)):
+        outs[f"attn{k}"] = rel_l2(a, r)[0]
+    grads, norms, n = {}, {}, 0
+    for k, p in m.named_parameters():
+        r = P[k].grad
+        n += 1
+        if r is None:
+            assert p.grad is None or p.grad.abs().max().item() == 0, k
+            continue
+        grads[k], norms[k] = rel_l2(p.grad, r)
+        norms[k] /= np.sqrt(r.numel())
+    assert n == len(list(m.parameters()))
+    floor = max(norms.values()) * 1e-2
+    for k in grads:
+        if norms[k] < floor:
+            grads[k] = grads[k] * norms[k] / floor
+    worst_out = max((e, k) for k, e in outs.items())
+    top = sorted(((e, k) for k, e in grads.items()), reverse=True)[:5]
+    print(f"configs[4] bf16 vs fp64: outputs {sorted(outs.items())}, worst gradients {top}")
+    assert worst_out[0] <= BF16_OUT_L2, worst_out
+    assert top[0][0] <= BF16_GRAD_L2, top

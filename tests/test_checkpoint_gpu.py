@@ -59,3 +59,42 @@ def test_window12_rename_format_checkpoint_into_tiny07_forward():
                            img.double(), "tiny07", max_depth=10.0)
     err = (depth - ref).abs().max().item()
     assert err <= 1e-4 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_training_state_resume_is_bit_exact(tmp_path, graph):
+    """save_checkpoint after 2 train steps of tiny07 (64x96, clipped AdamW, OneCycle), then 2
+    more steps, equals a fresh Trainer resumed from that file (Trainer.resume: weights,
+    FusedAdamW moments and per-parameter steps, OneCycle position) taking the same 2 steps --
+    bit for bit, eager and hipGraph-captured (utils/common_utils.py:12-31)."""
+    from mdemi.model.NewCRFs import NewCRFDepth
+    from mdemi.train import FusedAdamW, OneCycleLR, SILogLoss
+    from mdemi.train.builder import Trainer
+
+    g = torch.Generator().manual_seed(3)
+    data = [(torch.randn(2, 3, 64, 96, generator=g).to(DEV), (torch.rand(2, 1, 64, 96, generator=g) * 9 + 0.5).to(DEV))
+            for _ in range(4)]
+    loss = SILogLoss(10.0, 0.15)
+
+    def trainer(seed):
+        torch.manual_seed(seed)
+        m = NewCRFDepth(version="tiny07", max_depth=10.0, drop_path_rate=0.0).to(DEV).train()
+        opt = FusedAdamW(m.parameters(), lr=2e-4, weight_decay=0.01, max_grad_norm=0.1, capturable=graph)
+        sched = OneCycleLR(opt, max_lr=2e-4, total_steps=10, pct_start=0.3)
+        return Trainer({"train": {}}, m, loss, opt, sched, graph=graph)
+
+    a = trainer(0)
+    for i in range(2):
+        a.step([data[i]])
+    a.save("mid", str(tmp_path), 2, 0.0)
+    for i in range(2, 4):
+        a.step([data[i]])
+    b = trainer(1)
+    b.resume(str(tmp_path / "mid.pth"))
+    for i in range(2, 4):
+        b.step([data[i]])
+    torch.cuda.synchronize()
+    assert b.optimizer.step_count == a.optimizer.step_count == 4
+    assert b.scheduler.last_step == a.scheduler.last_step
+    for (k, pa), pb in zip(a.model.state_dict().items(), b.model.state_dict().values()):
+        assert torch.equal(pa, pb), k

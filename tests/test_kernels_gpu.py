@@ -545,36 +545,45 @@ def test_gemm_deep_split_skinny_wgrad(mf, M, N, K):
 def test_gemm_variants_bit_identical(mf, layouts):
     """Every pipelining variant (and hence the per-shape autotuner's pick) adds
     the k products in the same order: results must match bit for bit,
-    including split-K and a K that is not a multiple of 32."""
+    including split-K and a K that is not a multiple of 32 -- the register-staged
+    variants 0..7 and the direct-to-LDS variants 8..11 (gemm_glds_kernel.h) alike, with
+    the bias-gradient row sums of an m-contiguous A (wgrad) too.  A K that is not a
+    multiple of 4 cannot be staged by 16-B DMA: a forced direct-to-LDS variant falls back
+    to the register kernel and still agrees."""
     from mdemi import _lib as L
     lib = L.load()
-    M, N, K = 700, 300, 1000
-    a = torch.randn(M, K, device=DEV)
-    b = torch.randn(N, K, device=DEV)
-    at, bt = a.t().contiguous(), b.t().contiguous()
-    outs = []
-    try:
-        for v in range(8):
-            L.check(lib.mdemi_gemm_set_variant(v, 8), "set_variant")
-            for split in (1, 4, 5):
-                c = torch.empty(M, N, device=DEV)
-                if layouts == "fwd":
-                    mf.gemm(a, b, c, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
-                            split_k=split)
-                elif layouts == "dgrad":
-                    mf.gemm(a, bt, c, M, N, K, lda=K, ldb=N, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
-                            split_k=split)
-                else:
-                    mf.gemm(at, bt, c, M, N, K, lda=M, ldb=N, ldc=N, a_layout=L.L_MNCONTIG,
-                            b_layout=L.L_MNCONTIG, split_k=split)
-                outs.append((v, split, c))
-    finally:
-        lib.mdemi_gemm_set_variant(-1, 8)
-    ref = (a.double() @ b.double().t()).float()
-    for v, split, c in outs:
-        close(c, ref, rtol=1e-5 * math.sqrt(K))
-        same = [o for o in outs if o[1] == split][0][2]
-        assert torch.equal(c, same), f"variant {v} split {split} differs bitwise"
+    for M, N, K in ((700, 300, 1000), (520, 264, 999)):
+        a = torch.randn(M, K, device=DEV)
+        b = torch.randn(N, K, device=DEV)
+        at, bt = a.t().contiguous(), b.t().contiguous()
+        outs = []
+        try:
+            for v in range(12):
+                L.check(lib.mdemi_gemm_set_variant(v, 8), "set_variant")
+                for split in (1, 4, 5):
+                    c = torch.empty(M, N, device=DEV)
+                    rs = None
+                    if layouts == "fwd":
+                        mf.gemm(a, b, c, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+                                split_k=split)
+                    elif layouts == "dgrad":
+                        mf.gemm(a, bt, c, M, N, K, lda=K, ldb=N, ldc=N, a_layout=L.L_KCONTIG,
+                                b_layout=L.L_MNCONTIG, split_k=split)
+                    else:
+                        rs = torch.empty(M, device=DEV)
+                        mf.gemm(at, bt, c, M, N, K, lda=M, ldb=N, ldc=N, a_layout=L.L_MNCONTIG,
+                                b_layout=L.L_MNCONTIG, split_k=split, rowsum_a=rs)
+                    outs.append((v, split, c, rs))
+        finally:
+            lib.mdemi_gemm_set_variant(-1, 8)
+        ref = (a.double() @ b.double().t()).float()
+        for v, split, c, rs in outs:
+            close(c, ref, rtol=1e-5 * math.sqrt(K))
+            same = [o for o in outs if o[1] == split][0]
+            assert torch.equal(c, same[2]), f"variant {v} split {split} differs bitwise (K={K})"
+            if rs is not None:
+                close(rs, a.double().sum(1).float(), rtol=1e-5 * math.sqrt(K))
+                assert torch.equal(rs, same[3]), f"variant {v} split {split}: row sums differ bitwise (K={K})"
 
 
 @pytest.mark.parametrize("layouts", ["fwd", "dgrad"])
@@ -614,13 +623,31 @@ def test_gemm_tail_split(mf, layouts):
         lib.mdemi_gemm_set_options(1, 1)
     ref = (a.double() @ b.double().t() + bias.double() + res.double()).float()
     close(plain, ref, rtol=1e-5 * math.sqrt(K))
-    m_split = 8192  # (75 - ceil(264 / 24)) // 2 * 256 on a 256-CU device
+    m_split = _tail_plan_m_split(M, N, K, torch.cuda.get_device_properties(DEV).multi_processor_count)
+    assert m_split > 0, "the shape must leave a thin last round on this device"
     for v, c in outs:
         close(c, ref, rtol=1e-5 * math.sqrt(K))
         assert torch.equal(c, outs[0][1]), f"variant {v} differs bitwise with the tail split"
     c = outs[0][1]
     assert torch.equal(c[:m_split], plain[:m_split]), "rows above the cut must be the unsplit result"
     assert not torch.equal(c[m_split:], plain[m_split:]), "tail rows were not split (plan did not engage)"
+
+
+def _tail_plan_m_split(M, N, K, cus):
+    """Host restatement of gemm_f32.hip tail_plan (batch 1, split_k 1): the first split row,
+    0 when the plan does not engage.  The plan depends on the device's CU count, so which rows
+    are split over K -- and hence their fp32 summation order -- differs between GPU SKUs."""
+    cdiv = lambda a, b: -(-a // b)  # noqa: E731
+    tm, tn = cdiv(M, 128), cdiv(N, 128)
+    T, S = tm * tn, 3 * cus
+    full, rem = T // S, T % S
+    if full < 1 or rem == 0 or rem * 10 > S * 6:
+        return 0
+    m_split = (tm - cdiv(rem, tn)) // 2 * 256
+    if m_split <= 0:
+        return 0
+    s = min(4, S // (cdiv(M - m_split, 128) * tn), cdiv(K, 32) // 2)
+    return m_split if s >= 2 else 0
 
 
 @pytest.mark.parametrize("layouts", ["fwd", "wgrad"])

@@ -123,3 +123,59 @@ def test_optimizer_resume_after_capture(rccl):
     assert le == lg
     for (k, a), b in zip(eager.model.state_dict().items(), graph.model.state_dict().values()):
         assert torch.equal(a, b), k
+
+
+def test_capture_right_after_collectives(rccl):
+    """a global-mode capture begun right after eager collectives must not race the
+    process group's watchdog.  quiesce_process_group waits on the Works, then on
+    ProcessGroupNCCL::waitForPendingWorks (the watchdog's lists empty) -- a condition, not a
+    sleep -- and the capture that follows records and replays collectives correctly."""
+    from mdemi.train.builder import quiesce_process_group
+    ts = [torch.full((1 << 20,), float(i), device=DEV) for i in range(8)]
+    works = [dist.all_reduce(t, async_op=True) for t in ts]
+    quiesce_process_group(works)
+    x = torch.ones(4096, device=DEV)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = x * 2.0
+        dist.all_reduce(y)
+    for v in (1.0, 3.0):
+        x.fill_(v)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, torch.full_like(y, 2.0 * v))
+    for i, t in enumerate(ts):
+        assert torch.equal(t, torch.full_like(t, float(i)))
+
+
+def test_graph_captured_ddp_step_benchmark_size(rccl):
+    """BASELINE configs[4]'s own workload in the captured data-parallel step: Depthformer v8
+    (hidden 256, 256 bins, 256 aux tokens) at NYU 480x640, bf16, default 64 MB buckets on the
+    world-1 RCCL group, batch 2: the eager and the captured step agree bit for bit over 5 steps
+    (calls 1-2 eager, 3 captures, 3-5 replay) -- losses, every weight, the step counters."""
+    from mdemi.train import build_from_config
+    opt = _dfv8_opt(1)
+    opt["model"].update(hidden_dim=256, num_bins=256, num_aux=256, img_size=[480, 640])
+    torch.manual_seed(0)
+    eager = build_from_config(copy.deepcopy(opt), device=DEV, world=1, steps_per_epoch=20, precision="bf16",
+                              ddp=True)
+    torch.manual_seed(0)
+    graph = build_from_config(copy.deepcopy(opt), device=DEV, world=1, steps_per_epoch=20, precision="bf16",
+                              graph=True, ddp=True)
+    graph.model.load_state_dict(eager.model.state_dict())
+
+    def batch(seed):
+        g = torch.Generator().manual_seed(seed)
+        return (torch.randn(2, 3, 480, 640, generator=g).to(DEV),
+                (torch.rand(2, 1, 480, 640, generator=g) * 9.5 + 0.5).to(DEV))
+
+    le, lg = [], []
+    for s in range(5):
+        b = [batch(300 + s)]
+        le.append(eager.step(b).item())
+        lg.append(graph.step(b).item())
+    assert graph._graph is not None
+    assert le == lg, (le, lg)
+    for (k, a), b in zip(eager.model.state_dict().items(), graph.model.state_dict().values()):
+        assert torch.equal(a, b), k
+    assert graph.optimizer.steps == eager.optimizer.steps

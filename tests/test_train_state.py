@@ -1,0 +1,148 @@
+"""Training-state checkpoints (utils/common_utils.py:12-31 save_checkpoint) and resume,
+plus the loss-config validation (CPU only; no kernel runs).
+
+save_checkpoint writes the reference's file layout; load_checkpoint / Trainer.resume read
+it back (model weights, FusedAdamW moments and per-parameter step counts, epoch, OneCycle
+position).  The optimizer state is torch.optim.AdamW's layout, so a file written with the
+reference's torch AdamW resumes into FusedAdamW and ours loads into torch's."""
+import os
+import sys
+
+import pytest
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "monocular-depth-estimation_amd"))
+
+
+class _Tiny(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.encoder = torch.nn.Linear(4, 3)
+        self.head = torch.nn.Linear(3, 2)
+        self.bn = torch.nn.BatchNorm1d(2)
+
+
+def _torch_trained(seed=0, steps=3):
+    """A model + torch AdamW after `steps` steps (head gradients from step 2 only)."""
+    torch.manual_seed(seed)
+    m = _Tiny()
+    opt = torch.optim.AdamW([{"params": m.encoder.parameters(), "lr": 1e-4},
+                             {"params": list(m.head.parameters()) + list(m.bn.parameters()), "lr": 1e-3}],
+                            weight_decay=0.1)
+    for s in range(steps):
+        opt.zero_grad()
+        x = torch.randn(5, 4)
+        y = m.bn(m.head(m.encoder(x))) if s > 0 else m.encoder(x)
+        y.square().mean().backward()
+        opt.step()
+    return m, opt
+
+
+def test_save_checkpoint_file_layout(tmp_path):
+    from mdemi.train import FusedAdamW
+    from mdemi.utils.common_utils import CHECKPOINT_KEYS, save_checkpoint
+    m, topt = _torch_trained()
+    q = _Tiny()
+    q.load_state_dict(m.state_dict())
+    ours = FusedAdamW([{"params": q.encoder.parameters(), "lr": 1e-4},
+                       {"params": list(q.head.parameters()) + list(q.bn.parameters()), "lr": 1e-3}], weight_decay=0.1)
+    ours.load_state_dict(topt.state_dict())
+    save_checkpoint("ck", q, ours, 4, 123, 0.25, str(tmp_path))
+    ck = torch.load(tmp_path / "ck.pth", weights_only=True)
+    assert tuple(ck) == CHECKPOINT_KEYS
+    assert (ck["epoch"], ck["iter"], ck["best_epoch"], ck["best_iter"], ck["best"]) == (4, 123, 4, 123, 0.25)
+    assert ck["model_state_dict"].keys() == m.state_dict().keys()
+    # the optimizer state loads into the reference's torch AdamW unchanged
+    m2, _ = _torch_trained(seed=1, steps=0)
+    t2 = torch.optim.AdamW([{"params": m2.encoder.parameters(), "lr": 1e-4},
+                            {"params": list(m2.head.parameters()) + list(m2.bn.parameters()), "lr": 1e-3}],
+                           weight_decay=0.1)
+    t2.load_state_dict(ck["optimizer_state_dict"])
+    for p, p2 in zip(m.parameters(), m2.parameters()):
+        if p in topt.state:
+            assert float(t2.state[p2]["step"]) == float(topt.state[p]["step"])
+            assert torch.equal(t2.state[p2]["exp_avg"], topt.state[p]["exp_avg"])
+    save_checkpoint("mo", q, ours, 4, 123, 0.25, str(tmp_path), best_epoch=2, best_iter=60, model_only=True)
+    ck = torch.load(tmp_path / "mo.pth", weights_only=True)
+    assert ck["optimizer_state_dict"] is None and (ck["best_epoch"], ck["best_iter"]) == (2, 60)
+
+
+@pytest.mark.filterwarnings("ignore:Detected call of")
+def test_reference_written_checkpoint_resumes_trainer(tmp_path):
+    """A file in the reference's layout written with torch's AdamW (what the reference's
+    run would save) resumes a Trainer: weights, moments, per-parameter steps, epoch and the
+    OneCycle position (lr / beta1 of the next step equal torch's OneCycleLR after as many
+    optimizer steps)."""
+    from mdemi.train import FusedAdamW, OneCycleLR
+    from mdemi.train.builder import Trainer
+    m, topt = _torch_trained(steps=3)
+    total = 20
+    tsched = torch.optim.lr_scheduler.OneCycleLR(topt, max_lr=[1e-4, 1e-3], total_steps=total, pct_start=0.3,
+                                                 div_factor=25.0, final_div_factor=100.0)
+    for _ in range(3):
+        tsched.step()
+    torch.save({"epoch": 1, "iter": 3, "best_epoch": 1, "best_iter": 3, "model_state_dict": m.state_dict(),
+                "optimizer_state_dict": topt.state_dict(), "best": 0.5}, tmp_path / "ref.pth")
+    torch.manual_seed(7)
+    q = _Tiny()
+    opt = FusedAdamW([{"params": q.encoder.parameters(), "lr": 1e-4},
+                      {"params": list(q.head.parameters()) + list(q.bn.parameters()), "lr": 1e-3}], weight_decay=0.1)
+    sched = OneCycleLR(opt, max_lr=[1e-4, 1e-3], total_steps=total, pct_start=0.3, div_factor=25.0,
+                       final_div_factor=100.0)
+    tr = Trainer({"train": {}}, q, None, opt, sched)
+    ck = tr.resume(str(tmp_path / "ref.pth"))
+    assert ck["iter"] == 3 and tr.epoch == 1
+    for (k, a), b in zip(q.state_dict().items(), m.state_dict().values()):
+        assert torch.equal(a, b), k
+    assert opt.step_count == 3 and sorted(opt.steps) == [2, 2, 2, 2, 3, 3]
+    assert sched.last_step == 3
+    for g, tg in zip(opt.param_groups, topt.param_groups):
+        assert g["lr"] == pytest.approx(tg["lr"], rel=1e-12)
+        assert g["betas"][0] == pytest.approx(tg["betas"][0], rel=1e-12)
+    # and our save of the resumed state reads back identically
+    tr.save("again", str(tmp_path), 3, 0.5)
+    ck2 = torch.load(tmp_path / "again.pth", weights_only=True)
+    for i, st in ck2["optimizer_state_dict"]["state"].items():
+        assert torch.equal(st["exp_avg"], ck["optimizer_state_dict"]["state"][i]["exp_avg"])
+        assert float(st["step"]) == float(ck["optimizer_state_dict"]["state"][i]["step"])
+
+
+def test_load_checkpoint_errors(tmp_path):
+    from mdemi.train import FusedAdamW
+    from mdemi.utils.common_utils import load_checkpoint, save_checkpoint
+    q = _Tiny()
+    opt = FusedAdamW(q.parameters(), lr=1e-3)
+    torch.save({"state_dict": q.state_dict()}, tmp_path / "w.pth")
+    with pytest.raises(ValueError, match="not a save_checkpoint file"):
+        load_checkpoint(str(tmp_path / "w.pth"), q)
+    save_checkpoint("mo", q, opt, 0, 0, 0.0, str(tmp_path), model_only=True)
+    with pytest.raises(ValueError, match="model_only"):
+        load_checkpoint(str(tmp_path / "mo.pth"), q, opt)
+
+
+def test_onecycle_set_position_matches_stepping():
+    from mdemi.train import FusedAdamW, OneCycleLR
+    p = torch.nn.Parameter(torch.zeros(2))
+    a = OneCycleLR(FusedAdamW([p], lr=1e-3), max_lr=1e-3, total_steps=30)
+    b = OneCycleLR(FusedAdamW([torch.nn.Parameter(torch.zeros(2))], lr=1e-3), max_lr=1e-3, total_steps=30)
+    for s in range(1, 30):
+        a.step()
+        b.set_position(s)
+        assert a.opt.param_groups[0]["lr"] == b.opt.param_groups[0]["lr"]
+        assert a.opt.param_groups[0]["betas"] == b.opt.param_groups[0]["betas"]
+    with pytest.raises(ValueError):
+        b.set_position(31)
+
+
+@pytest.mark.parametrize("loss,err", [({"sog_weight": 0.5, "reduction_ratio": 8}, "sog_weight"),
+                                      ({"focal_gamma": 2.0}, "not implemented"),
+                                      ({"sog_weight": 0.0, "reduction_ratio": 8}, None)])
+def test_loss_keys_are_validated(loss, err):
+    from mdemi.train.builder import TrainLoss
+    opt = {"loss": dict(alpha=10.0, beta=0.15, per_image=True, **loss), "eval": {"min_depth_eval": 1e-3}}
+    if err is None:
+        TrainLoss(opt, "oda2_red_order_swin2")
+    else:
+        with pytest.raises(ValueError, match=err):
+            TrainLoss(opt, "oda2_red_order_swin2")
