@@ -380,13 +380,16 @@ typedef struct mdemi_adamw_group {
  * follow.  tensors_dev is a device array of mdemi_tensor_ref. */
 int mdemi_multi_tensor_chunk(void);
 size_t mdemi_grad_norm_workspace_size(int32_t nitems);
-/* sumsq[0] <- sum over tensors of ||grad||^2 (deterministic two-level sum) */
+/* sumsq[0] <- sum over tensors of ||grad_scale * grad||^2 (deterministic two-level sum).
+ * grad_scale (> 0) is the factor every gradient is taken at, in this norm and in the
+ * update below: 1/world folds the data-parallel mean into the optimizer (the summed
+ * gradients of the all-reduce are never swept just to scale them); 1 otherwise. */
 int mdemi_grad_sumsq(const mdemi_tensor_ref* tensors_dev, int32_t ntensors, int64_t nitems,
-                     float* sumsq, void* workspace, void* stream);
+                     float grad_scale, float* sumsq, void* workspace, void* stream);
 /* One AdamW step (torch.optim.AdamW semantics, decoupled weight decay).
  * groups_host: up to 4 parameter groups (host memory, passed by value).
  * step: 1-based step count for bias correction.  max_norm <= 0 disables the
- * clip; otherwise grads are scaled by min(1, max_norm / (sqrt(sumsq)+1e-6)),
+ * clip; otherwise grads (times grad_scale) are scaled by min(1, max_norm / (sqrt(sumsq)+1e-6)),
  * as torch.nn.utils.clip_grad_norm_ does, without a host round trip.
  * tensor_steps (device, optional): per-parameter step counters, torch's
  * state[p]["step"] -- a parameter whose gradient first appears late has its own
@@ -395,8 +398,8 @@ int mdemi_grad_sumsq(const mdemi_tensor_ref* tensors_dev, int32_t ntensors, int6
  * increments tensor_steps[t.step_slot] for every tensor in the table. */
 int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                      const mdemi_adamw_group* groups_host, int32_t ngroups,
-                     const float* sumsq, float max_norm, int32_t step, int32_t* tensor_steps,
-                     int64_t nitems, void* workspace, void* stream);
+                     const float* sumsq, float max_norm, float grad_scale, int32_t step,
+                     int32_t* tensor_steps, int64_t nitems, void* workspace, void* stream);
 /* Capturable form (a hipGraph-captured train step): the hyperparameters come
  * from device memory.  sched_dev is a [nsteps][ngroups] table of
  * mdemi_adamw_group entries -- e.g. the OneCycle lr / beta1 of every optimizer step --
@@ -408,7 +411,7 @@ int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
 int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                          const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
                          int32_t* step_dev, int32_t* tensor_steps, const float* sumsq, float max_norm,
-                         int64_t nitems, void* workspace, void* stream);
+                         float grad_scale, int64_t nitems, void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

@@ -48,7 +48,22 @@ struct GemmParams {
   // tiles), as is every tile of an ordinary split-K GEMM (tiles_m1 = 0).
   int tiles_m1, m_split;
   int* tile_cnt;  // non-null: the last-arriving split of a tile combines the slabs (no reduce launch)
+  float* rowsum_out;  // with tile_cnt and split row-sum partials: the last arriver writes the sums here
 };
+
+// One thread's 4 bias-gradient row sums (rows i..i+3) of a K piece: plain stores, or
+// write-through (sc1) stores when the pieces are split (the tile's last arriver may read
+// them in this launch, gemm_epilogue.inc).
+__device__ __forceinline__ void store_rowsum4(const GemmParams& p, int sidx, int i, float4 s4) {
+  float* dst = p.rowsum + (p.split > 1 ? (int64_t)sidx * p.M : 0);
+  const float v[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (i + e >= p.M) break;
+    if (p.split > 1) __hip_atomic_store(dst + i + e, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else dst[i + e] = v[e];
+  }
+}
 
 // element offset of batch entry b of an operand with outer stride s, inner stride s2
 __device__ __forceinline__ int64_t boff(const GemmParams& p, int b, int64_t s, int64_t s2) {

@@ -139,7 +139,7 @@ static int variant_bk(int v, int mode) {
   return (v >= 3 && v != 7) ? 32 : 16;
 }
 static int variant_rows(int v, int mode) {
-  return (mode != GEMM_F32 ? v == 2 : (v == 6 || v == 7 || v == 9 || v == 10)) ? 2 * GBM : GBM;
+  return (mode != GEMM_F32 ? (v == 2 || v == 4) : (v == 6 || v == 7 || v == 9 || v == 10)) ? 2 * GBM : GBM;
 }
 // the direct-to-LDS variants need dense operands that load as whole 16-B quads and no
 // load-time transform
@@ -262,6 +262,7 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
   p.split = (int)cdiv(kc, chunks_per_split);
   p.m_split = (tp.split > 1 && p.split > 1) ? tp.m_split : 0;
   p.tile_cnt = nullptr;
+  p.rowsum_out = nullptr;
   // vector loads need every row start 16-B aligned and whole quads in range
   // (KCONTIG: K % 4; MNCONTIG: the row/column extent % 4)
   p.a_vec = al16(d->A) && (d->lda % 4 == 0) && (d->a_bstride % 4 == 0) && (p.a_bs2 % 4 == 0) &&
@@ -327,6 +328,7 @@ static size_t colsum_combine_bytes(const mdemi_gemm_desc* d, const GemmParams& p
 }
 
 static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mode) {
+  if (mode == GEMM_F32E && variant >= 3) variant = 0;  // the bf16-image variants hold one bf16 plane
   if (mode == GEMM_F32 && variant >= 8) {  // a forced direct-to-LDS variant on an operand it cannot stage
     GemmParams q;
     fill_params(d, q, variant, mode);
@@ -358,8 +360,10 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mod
   const int64_t nblocks = (int64_t)p.tiles_m1 * p.tiles_n + (int64_t)p.tiles_m * p.tiles_n * d->batch * p.split;
   MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
   const bool deep = p.split > 1 && colsum_combine(d, p);
-  if (p.split > 1 && !deep && !rowsum_part && (g_inline_reduce || p.m_split > 0))
+  if (p.split > 1 && !deep && (g_inline_reduce || p.m_split > 0)) {
     p.tile_cnt = tile_counters((int64_t)p.tiles_m * p.tiles_n * d->batch, st);
+    if (p.tile_cnt && rowsum_part) p.rowsum_out = d->rowsum_a;  // the last arrivers sum the row partials
+  }
   hipLaunchKernelGGL(fn, dim3((unsigned)nblocks), dim3(GTHREADS), 0, st, p);
   if (p.split > 1 && !p.tile_cnt) {
     if (deep) {
@@ -411,9 +415,9 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
   }
   if (!tunable(d, st)) return 0;
   static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11};
-  static const int cands_m16[] = {0, 1, 2};
+  static const int cands_m16[] = {0, 1, 2, 3, 4};
   const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
-  int ncand = mode != GEMM_F32 ? 3 : 11;
+  int ncand = mode == GEMM_BF16 ? 5 : mode == GEMM_F32E ? 3 : 11;
   if (mode == GEMM_F32) {
     GemmParams q;
     fill_params(d, q, 0, mode);
@@ -477,7 +481,7 @@ extern "C" int mdemi_gemm_set_options(int32_t tail_split, int32_t inline_reduce)
 }
 
 extern "C" int mdemi_gemm_set_variant_m16(int32_t variant) {
-  MDEMI_REQUIRE(variant >= -1 && variant < 3, "gemm_set_variant_m16: bad variant");
+  MDEMI_REQUIRE(variant >= -1 && variant < 5, "gemm_set_variant_m16: bad variant");
   g_variant_m16 = variant;
   return MDEMI_OK;
 }

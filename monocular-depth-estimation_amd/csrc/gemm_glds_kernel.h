@@ -242,14 +242,8 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
         const float4 o = red[a * 256 + tt + 32 * g];
         s4.x += o.x; s4.y += o.y; s4.z += o.z; s4.w += o.w;
       }
-      float* dst = p.rowsum + (p.split > 1 ? (int64_t)sidx * p.M : 0);
-      const int i = bm + 128 * a + 4 * tt;
-      if (i + 0 < p.M) dst[i + 0] = s4.x;
-      if (i + 1 < p.M) dst[i + 1] = s4.y;
-      if (i + 2 < p.M) dst[i + 2] = s4.z;
-      if (i + 3 < p.M) dst[i + 3] = s4.w;
+      store_rowsum4(p, sidx, bm + 128 * a + 4 * tt, s4);
     }
-    __syncthreads();  // the epilogue's hand-off flag reuses smem
   }
 
 #define EP_IM IM

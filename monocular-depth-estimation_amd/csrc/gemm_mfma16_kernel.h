@@ -69,6 +69,41 @@ __device__ __forceinline__ void f32_store(float* img, int t, const float4 (&r)[M
   }
 }
 
+// ---- bf16 images (variants 3, 4; NP = 1): operands rounded once, as they are staged ----
+// [row][32 k] bf16, 64 B per row, 16-B chunks (8 k) permuted by chunk ^ ((row >> 2) & 3):
+// the fragment reads (ds_read_b128, 8 k of one row per lane) are conflict free.
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+constexpr int BF_ROW = M16_BK * 2;  // bytes per image row
+__device__ __forceinline__ int bf_swz(int row) { return (row >> 2) & 3; }
+__device__ __forceinline__ uint2 pack_bf16x4(float a, float b, float c, float d) {
+  const bf16x2_t lo = __builtin_convertvector((float2_t){a, b}, bf16x2_t);
+  const bf16x2_t hi = __builtin_convertvector((float2_t){c, d}, bf16x2_t);
+  const bf16x4_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3);
+  return *reinterpret_cast<const uint2*>(&v);
+}
+// 4 consecutive k (quad kq = 0..7 of the 32) of image row `row`, rounded to bf16, as 8 B
+__device__ __forceinline__ void bf_put(char* img, int row, int kq, uint2 v) {
+  *reinterpret_cast<uint2*>(img + row * BF_ROW + (((kq >> 1) ^ bf_swz(row)) << 4) + ((kq & 1) << 3)) = v;
+}
+template <int IMG>
+__device__ __forceinline__ void bf16_store(char* img, int t, const float4 (&r)[M16_BK / 8]) {
+  if constexpr (IMG == IMG_KR) {  // KC loader: r[q] = columns 4*(t&31)..+3 at k = 4*(t>>5) + q
+    const int c4 = t & 31, kq = t >> 5;
+    bf_put(img, 4 * c4 + 0, kq, pack_bf16x4(r[0].x, r[1].x, r[2].x, r[3].x));
+    bf_put(img, 4 * c4 + 1, kq, pack_bf16x4(r[0].y, r[1].y, r[2].y, r[3].y));
+    bf_put(img, 4 * c4 + 2, kq, pack_bf16x4(r[0].z, r[1].z, r[2].z, r[3].z));
+    bf_put(img, 4 * c4 + 3, kq, pack_bf16x4(r[0].w, r[1].w, r[2].w, r[3].w));
+  } else {  // row t/8 + 32q, k quad t%8
+#pragma unroll
+    for (int q = 0; q < M16_BK / 8; ++q)
+      bf_put(img, (t >> 3) + 32 * q, t & 7, pack_bf16x4(r[q].x, r[q].y, r[q].z, r[q].w));
+  }
+}
+// MFMA k-step kk's fragment (k = 16 kk + 8 h .. +7) of image row `row`
+__device__ __forceinline__ bf16x8_t bf_frag(const char* img, int row, int kk, int h) {
+  return *reinterpret_cast<const bf16x8_t*>(img + row * BF_ROW + (((2 * kk + h) ^ bf_swz(row)) << 4));
+}
+
 // 8 fp32 (k .. k+7 of one row) -> NP bf16x8 operand fragments: out[0] = RNE bf16 of the
 // values, out[p] = RNE bf16 of what the planes before it leave (exact fp32 remainders)
 template <int NP>
@@ -91,15 +126,19 @@ __device__ __forceinline__ void split8(const float4& u, const float4& v, bf16x8_
 
 // BMT: block tile rows (128: 2x2 waves of 64x64; 256: 2x2 waves of 128x64, A staged
 // as two 128-row images).  The block tile is 128 columns wide.
-template <int AL, int BL, int AOP, int BOP, int NP, int NBUF, int BMT>
+// BFL: operands rounded to bf16 as they are staged (bf16 LDS images, half the LDS bytes and
+// one conversion per element instead of one per reading wave); NP = 1 only.  Same bf16
+// values in the same MFMA positions as the fp32-image form: bit-identical results.
+template <int AL, int BL, int AOP, int BOP, int NP, int NBUF, int BMT, bool BFL = false>
 __global__ __launch_bounds__(GTHREADS) void gemm_m16_kernel(GemmParams p) {
+  static_assert(!BFL || NP == 1, "bf16 LDS images hold one plane");
   constexpr int BK = M16_BK, NQ = BK / 8;
   constexpr int NA = BMT / 128;     // 128-row A images per tile
   constexpr int IM = BMT / 64;      // 32-row accumulator blocks per wave along M
   constexpr int WTM = BMT / 2;      // wave tile rows
   using LA = Loader<AL, AOP, true, BK, false, true>;
   using LB = Loader<BL, BOP, false, BK, false, true>;
-  constexpr int IMG_B = GBM * F32_PITCH * 4;  // bytes of one 128-row fp32 image
+  constexpr int IMG_B = BFL ? GBM * BF_ROW : GBM * F32_PITCH * 4;  // bytes of one 128-row image
   constexpr int BUF_B = (NA + 1) * IMG_B;     // A images + the B image
   static_assert(NBUF == 1 || NBUF == 2, "NBUF");
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF_B];
@@ -160,12 +199,35 @@ __global__ __launch_bounds__(GTHREADS) void gemm_m16_kernel(GemmParams p) {
     lb.load(kt * BK, rb);
   };
   auto stage = [&](char* dst) {
+    if constexpr (BFL) {
 #pragma unroll
-    for (int a = 0; a < NA; ++a) f32_store<LA::IMG>(reinterpret_cast<float*>(dst + a * IMG_B), t, ra[a]);
-    f32_store<LB::IMG>(reinterpret_cast<float*>(dst + NA * IMG_B), t, rb);
+      for (int a = 0; a < NA; ++a) bf16_store<LA::IMG>(dst + a * IMG_B, t, ra[a]);
+      bf16_store<LB::IMG>(dst + NA * IMG_B, t, rb);
+    } else {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) f32_store<LA::IMG>(reinterpret_cast<float*>(dst + a * IMG_B), t, ra[a]);
+      f32_store<LB::IMG>(reinterpret_cast<float*>(dst + NA * IMG_B), t, rb);
+    }
     acc_rsum();
   };
   auto compute = [&](const char* buf) {
+    if constexpr (BFL) {
+      const char* a_s = buf + aimg * IMG_B;
+      const char* b_s = buf + NA * IMG_B;
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        bf16x8_t A[IM], B[2];
+#pragma unroll
+        for (int i = 0; i < IM; ++i) A[i] = bf_frag(a_s, rA[i], kk, h);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) B[i] = bf_frag(b_s, rB[i], kk, h);
+#pragma unroll
+        for (int im = 0; im < IM; ++im)
+#pragma unroll
+          for (int in = 0; in < 2; ++in) MDEMI_MFMA16(A[im], B[in], acc[im][in]);
+      }
+      return;
+    }
     const float* a_s = reinterpret_cast<const float*>(buf + aimg * IMG_B);
     const float* b_s = reinterpret_cast<const float*>(buf + NA * IMG_B);
 #pragma unroll
@@ -241,12 +303,7 @@ __global__ __launch_bounds__(GTHREADS) void gemm_m16_kernel(GemmParams p) {
         const float4 o = red[a * 256 + tt + 32 * g];
         s4.x += o.x; s4.y += o.y; s4.z += o.z; s4.w += o.w;
       }
-      float* dst = p.rowsum + (p.split > 1 ? (int64_t)sidx * p.M : 0);
-      const int i = bm + 128 * a + 4 * tt;
-      if (i + 0 < p.M) dst[i + 0] = s4.x;
-      if (i + 1 < p.M) dst[i + 1] = s4.y;
-      if (i + 2 < p.M) dst[i + 2] = s4.z;
-      if (i + 3 < p.M) dst[i + 3] = s4.w;
+      store_rowsum4(p, sidx, bm + 128 * a + 4 * tt, s4);
     }
   }
 #define EP_IM IM
@@ -258,10 +315,15 @@ __global__ __launch_bounds__(GTHREADS) void gemm_m16_kernel(GemmParams p) {
 using KernelFn16 = void (*)(GemmParams);
 
 // 16-bit family variants: 0 = 128-row tile, two LDS buffers; 1 = 128-row tile, one
-// buffer (two workgroups per CU by LDS); 2 = 256-row tile, two buffers (96 KiB).
+// buffer (two workgroups per CU by LDS); 2 = 256-row tile, two buffers (96 KiB);
+// 3 / 4 = bf16 LDS images (bf16 only), 128- / 256-row tile, two buffers (32 / 48 KiB).
 // Every variant adds each output's products in the same order (bit-identical).
 template <int AL, int BL, int AOP, int BOP>
 static KernelFn16 m16_variant(int np, int v) {
+  if (v >= 3) {  // bf16 LDS images (NP = 1): 3 = 128-row tile, 4 = 256-row tile, two buffers each
+    if (np != 1) return nullptr;
+    return v == 4 ? gemm_m16_kernel<AL, BL, AOP, BOP, 1, 2, 256, true> : gemm_m16_kernel<AL, BL, AOP, BOP, 1, 2, 128, true>;
+  }
   if (np == 3) {
     if (v == 2) return gemm_m16_kernel<AL, BL, AOP, BOP, 3, 2, 256>;
     return v == 1 ? gemm_m16_kernel<AL, BL, AOP, BOP, 3, 1, 128> : gemm_m16_kernel<AL, BL, AOP, BOP, 3, 2, 128>;

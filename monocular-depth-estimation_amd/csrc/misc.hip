@@ -111,13 +111,20 @@ struct AdamGroups {
   mdemi_adamw_group g[4];
 };
 
+// gradients as the update sees them: g * gs (gs = 1/world when the data-parallel mean's
+// scale is folded in here instead of a sweep over the reduced gradients; 1 otherwise)
+__device__ __forceinline__ float4 scale4(float4 g, float gs) {
+  if (gs != 1.f) { g.x *= gs; g.y *= gs; g.z *= gs; g.w *= gs; }
+  return g;
+}
+
 // per-tensor sum of squares partials: one block per (tensor, chunk); float4
 // loads over the 16-B-aligned body of the chunk (torch allocations are 256-B
 // aligned and chunks are multiples of 4 elements), scalar tail
 __global__ __launch_bounds__(OPT_THREADS) void sumsq_partial(const mdemi_tensor_ref* __restrict__ tl, int nt,
                                                              const int* __restrict__ chunk_tensor,
                                                              const int* __restrict__ chunk_index,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part, float gs) {
   __shared__ float red[OPT_THREADS / 64];
   const int item = blockIdx.x;
   const mdemi_tensor_ref t = tl[chunk_tensor[item]];
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(OPT_THREADS) void sumsq_partial(const mdemi_tensor_
   for (; i + 3 * STEP < vend; i += 4 * STEP) {
     float4 g[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) g[u] = *reinterpret_cast<const float4*>(t.grad + i + u * STEP);
+    for (int u = 0; u < 4; ++u) g[u] = scale4(*reinterpret_cast<const float4*>(t.grad + i + u * STEP), gs);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       s4[u] = fmaf(g[u].x, g[u].x, s4[u]); s4[u] = fmaf(g[u].y, g[u].y, s4[u]);
@@ -140,11 +147,14 @@ __global__ __launch_bounds__(OPT_THREADS) void sumsq_partial(const mdemi_tensor_
     }
   }
   for (; i < vend; i += STEP) {
-    const float4 g = *reinterpret_cast<const float4*>(t.grad + i);
+    const float4 g = scale4(*reinterpret_cast<const float4*>(t.grad + i), gs);
     s4[0] = fmaf(g.x, g.x, s4[0]); s4[0] = fmaf(g.y, g.y, s4[0]);
     s4[0] = fmaf(g.z, g.z, s4[0]); s4[0] = fmaf(g.w, g.w, s4[0]);
   }
-  for (int64_t j = vend + threadIdx.x; j < end; j += OPT_THREADS) s4[1] = fmaf(t.grad[j], t.grad[j], s4[1]);
+  for (int64_t j = vend + threadIdx.x; j < end; j += OPT_THREADS) {
+    const float g = gs != 1.f ? t.grad[j] * gs : t.grad[j];
+    s4[1] = fmaf(g, g, s4[1]);
+  }
   float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   s = block_sum<OPT_THREADS>(s, red);
   if (threadIdx.x == 0) part[item] = s;
@@ -166,12 +176,13 @@ __global__ void sumsq_final(const float* __restrict__ part, int nitems, float* _
 // torch.optim.AdamW on one (tensor, chunk) item (decoupled weight decay,
 // non-amsgrad, foreach=False semantics); `step` is the 1-based step count
 __device__ __forceinline__ void adamw_item(const mdemi_tensor_ref& t, const mdemi_adamw_group& gp, float clip,
-                                           float step, int64_t beg, int64_t end) {
+                                           float gs, float step, int64_t beg, int64_t end) {
   const float b1 = gp.beta1, b2 = gp.beta2;
   const float step_size = gp.lr / (1.f - powf(b1, step));
   const float bc2s = sqrtf(1.f - powf(b2, step));
   const float decay = 1.f - gp.lr * gp.weight_decay;
   auto upd = [&](float g, float& p, float& m, float& v) {
+    if (gs != 1.f) g *= gs;
     g *= clip;
     p *= decay;
     m = m * b1 + (1.f - b1) * g;
@@ -202,13 +213,13 @@ __device__ __forceinline__ float clip_coef(const float* sumsq, float max_norm) {
 __global__ __launch_bounds__(OPT_THREADS) void adamw_kernel(const mdemi_tensor_ref* __restrict__ tl,
                                                             const int* __restrict__ chunk_tensor,
                                                             const int* __restrict__ chunk_index, AdamGroups groups,
-                                                            const float* __restrict__ sumsq, float max_norm, int step,
-                                                            const int* __restrict__ tensor_steps) {
+                                                            const float* __restrict__ sumsq, float max_norm, float gs,
+                                                            int step, const int* __restrict__ tensor_steps) {
   const int item = blockIdx.x;
   const mdemi_tensor_ref t = tl[chunk_tensor[item]];
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
   const int s = tensor_steps ? tensor_steps[t.step_slot] + 1 : step;
-  adamw_item(t, groups.g[t.group], clip_coef(sumsq, max_norm), (float)s, beg, min(t.numel, beg + OPT_CHUNK));
+  adamw_item(t, groups.g[t.group], clip_coef(sumsq, max_norm), gs, (float)s, beg, min(t.numel, beg + OPT_CHUNK));
 }
 
 // capturable form: hyperparameters of step s (= *step_dev, steps already taken)
@@ -220,14 +231,15 @@ __global__ __launch_bounds__(OPT_THREADS) void adamw_dev_kernel(const mdemi_tens
                                                                 int nsteps, int ngroups,
                                                                 const int* __restrict__ step_dev,
                                                                 const int* __restrict__ tensor_steps,
-                                                                const float* __restrict__ sumsq, float max_norm) {
+                                                                const float* __restrict__ sumsq, float max_norm,
+                                                                float gs) {
   const int item = blockIdx.x;
   const mdemi_tensor_ref t = tl[chunk_tensor[item]];
   const int s = step_dev[0];
   const mdemi_adamw_group gp = sched[(int64_t)min(s, nsteps - 1) * ngroups + t.group];
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
   const int bc = tensor_steps ? tensor_steps[t.step_slot] + 1 : s + 1;
-  adamw_item(t, gp, clip_coef(sumsq, max_norm), (float)bc, beg, min(t.numel, beg + OPT_CHUNK));
+  adamw_item(t, gp, clip_coef(sumsq, max_norm), gs, (float)bc, beg, min(t.numel, beg + OPT_CHUNK));
 }
 
 // after the update: advance the optimizer's step counter and/or every listed
@@ -298,25 +310,26 @@ extern "C" size_t mdemi_grad_norm_workspace_size(int32_t nitems) {
 
 extern "C" int mdemi_multi_tensor_chunk(void) { return OPT_CHUNK; }
 
-extern "C" int mdemi_grad_sumsq(const mdemi_tensor_ref* tensors_dev, int32_t ntensors, int64_t nitems, float* sumsq,
-                                void* workspace, void* stream) {
-  MDEMI_REQUIRE(tensors_dev && ntensors > 0 && nitems > 0 && sumsq && workspace, "grad_sumsq: bad args");
+extern "C" int mdemi_grad_sumsq(const mdemi_tensor_ref* tensors_dev, int32_t ntensors, int64_t nitems,
+                                float grad_scale, float* sumsq, void* workspace, void* stream) {
+  MDEMI_REQUIRE(tensors_dev && ntensors > 0 && nitems > 0 && sumsq && workspace && grad_scale > 0.f,
+                "grad_sumsq: bad args");
   const int* ct = (const int*)workspace;
   const int* ci = ct + nitems;
   float* part = (float*)(ci + nitems);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(sumsq_partial, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, st, tensors_dev, ntensors, ct, ci,
-                     part);
+                     part, grad_scale);
   hipLaunchKernelGGL(sumsq_final, dim3(1), dim3(256), 0, st, part, (int)nitems, sumsq);
   return check_launch("grad_sumsq");
 }
 
 extern "C" int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                                 const mdemi_adamw_group* groups_host, int32_t ngroups, const float* sumsq,
-                                float max_norm, int32_t step, int32_t* tensor_steps, int64_t nitems, void* workspace,
-                                void* stream) {
+                                float max_norm, float grad_scale, int32_t step, int32_t* tensor_steps, int64_t nitems,
+                                void* workspace, void* stream) {
   MDEMI_REQUIRE(tensors_dev && ntensors > 0 && groups_host && ngroups > 0 && ngroups <= 4 &&
-                    (step >= 1 || tensor_steps) && nitems > 0 && workspace,
+                    (step >= 1 || tensor_steps) && nitems > 0 && workspace && grad_scale > 0.f,
                 "adamw_step: bad args");
   AdamGroups g;
   for (int i = 0; i < ngroups; ++i) g.g[i] = groups_host[i];
@@ -325,7 +338,7 @@ extern "C" int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t nte
   const int* ci = ct + nitems;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, st, tensors_dev, ct, ci, g, sumsq,
-                     max_norm, step, (const int*)tensor_steps);
+                     max_norm, grad_scale, step, (const int*)tensor_steps);
   if (tensor_steps)
     hipLaunchKernelGGL(step_tick_kernel, dim3((unsigned)cdiv(ntensors, 256)), dim3(256), 0, st, (int*)nullptr,
                        tensors_dev, ntensors, (int*)tensor_steps);
@@ -335,15 +348,15 @@ extern "C" int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t nte
 extern "C" int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                                     const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
                                     int32_t* step_dev, int32_t* tensor_steps, const float* sumsq, float max_norm,
-                                    int64_t nitems, void* workspace, void* stream) {
+                                    float grad_scale, int64_t nitems, void* workspace, void* stream) {
   MDEMI_REQUIRE(tensors_dev && ntensors > 0 && sched_dev && nsteps > 0 && ngroups > 0 && ngroups <= 4 && step_dev &&
-                    nitems > 0 && workspace,
+                    nitems > 0 && workspace && grad_scale > 0.f,
                 "adamw_step_dev: bad args");
   const int* ct = (const int*)workspace;
   const int* ci = ct + nitems;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(adamw_dev_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, st, tensors_dev, ct, ci, sched_dev,
-                     nsteps, ngroups, (const int*)step_dev, (const int*)tensor_steps, sumsq, max_norm);
+                     nsteps, ngroups, (const int*)step_dev, (const int*)tensor_steps, sumsq, max_norm, grad_scale);
   hipLaunchKernelGGL(step_tick_kernel, dim3((unsigned)cdiv(ntensors, 256)), dim3(256), 0, st, (int*)step_dev,
                      tensors_dev, ntensors, (int*)tensor_steps);
   return check_launch("adamw_step_dev");

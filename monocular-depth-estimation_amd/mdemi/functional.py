@@ -426,7 +426,7 @@ class _Conv2dFn(torch.autograd.Function):
                 dx = torch.empty_like(x)
                 if pad_mode == L.PAD_ZERO:
                     gemm(dy, wd, dx, n * h * w, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
-                         b_layout=L.L_MNCONTIG, split_k=1,
+                         b_layout=L.L_MNCONTIG,
                          conv=_geom(n, oh, ow, cout, h, w, kh, kw, 1, kh - 1 - pad, L.PAD_ZERO))
                 else:
                     # replicate padding (layer_utils.py:21): gradient of the padded input by a full
@@ -434,7 +434,7 @@ class _Conv2dFn(torch.autograd.Function):
                     hp, wp = h + 2 * pad, w + 2 * pad
                     dxp = torch.empty(n, hp, wp, c, device=dy.device, dtype=torch.float32)
                     gemm(dy, wd, dxp, n * hp * wp, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
-                         b_layout=L.L_MNCONTIG, split_k=1,
+                         b_layout=L.L_MNCONTIG,
                          conv=_geom(n, oh, ow, cout, hp, wp, kh, kw, 1, kh - 1, L.PAD_ZERO))
                     L.call("mdemi_pad_fold_replicate", dxp.data_ptr(), dx.data_ptr(), n, h, w, c, pad, L.stream())
         want_db = has_bias and ctx.needs_input_grad[2]

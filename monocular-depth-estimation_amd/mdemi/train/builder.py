@@ -234,6 +234,11 @@ class Trainer:
         self._graph = None
         self._graph_layout = None
         self._eager_calls = 0
+        if ddp is not None and ddp.world > 1 and hasattr(optimizer, "grad_scale"):
+            # the all-reduce leaves gradient sums; the AdamW step takes them at 1/world (its
+            # clip norm too), bit for bit what scaling the buckets first would give
+            ddp.scale_in_finish = False
+            optimizer.grad_scale = 1.0 / ddp.world
 
     def train_mode(self):
         self.model.train()

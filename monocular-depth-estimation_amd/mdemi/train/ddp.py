@@ -20,7 +20,9 @@ autograd engine fires hooks in.  Each launch is an async all-reduce (SUM) on
 torch.distributed's communication stream — backend "nccl" is RCCL over xGMI
 on ROCm — overlapping the rest of the backward.  ``finish()`` waits for the
 outstanding collectives and scales each bucket by 1/world in place (one
-libmdemi sweep per bucket).  Inside ``no_sync()`` the hooks only let
+libmdemi sweep per bucket) -- unless ``scale_in_finish`` is off: mdemi's
+Trainer folds 1/world into the optimizer step instead (FusedAdamW.grad_scale),
+so the reduced sums are never swept just to be scaled.  Inside ``no_sync()`` the hooks only let
 gradients accumulate; the reduction happens on the first backward outside it.
 
 If something replaced a ``.grad`` (``zero_grad(set_to_none=True)``, a first
@@ -39,6 +41,9 @@ class GradAllReduce:
 
     def __init__(self, model, bucket_mb: float = 64.0, group=None):
         self.group = group
+        # finish() turns the sums into means in place; a consumer that applies 1/world itself
+        # (FusedAdamW.grad_scale, wired by Trainer) sets this False and saves that sweep
+        self.scale_in_finish = True
         self.world = dist.get_world_size(group)
         self.params = [p for p in model.parameters() if p.requires_grad]
         if not self.params:
@@ -151,7 +156,7 @@ class GradAllReduce:
             raise RuntimeError(f"GradAllReduce: buckets {missing} never completed (unused parameters?)")
         for w in self._works:
             w.wait()
-        if self.world > 1:
+        if self.world > 1 and self.scale_in_finish:
             for flat in self.flat:
                 self._scale(flat, 1.0 / self.world)
         for p in self.params:  # an optimizer may have replaced a view meanwhile

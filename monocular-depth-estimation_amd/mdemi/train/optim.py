@@ -48,6 +48,10 @@ class FusedAdamW:
         if len(self.param_groups) > 4:
             raise ValueError("FusedAdamW: at most 4 parameter groups")
         self.max_grad_norm = float(max_grad_norm)
+        # every gradient is taken at grad_scale x its value, in the clip norm and the update
+        # (Trainer sets 1/world when the data-parallel all-reduce leaves sums: the mean's
+        # scale rides on this step instead of a separate sweep over the gradients)
+        self.grad_scale = 1.0
         self.state = {}
         self.step_count = 0  # optimizer steps taken (the schedule position)
         self._slot = {}
@@ -173,21 +177,22 @@ class FusedAdamW:
             self._steps_dev = torch.tensor(self.steps, dtype=torch.int32).to(dev)
         if self._sumsq is None:
             self._sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
+        gs = float(self.grad_scale)
         if self.max_grad_norm > 0:
-            L.check(lib.mdemi_grad_sumsq(tl_ptr, nt, ni, self._sumsq.data_ptr(), ws_ptr, L.stream()), "grad_sumsq")
+            L.check(lib.mdemi_grad_sumsq(tl_ptr, nt, ni, gs, self._sumsq.data_ptr(), ws_ptr, L.stream()), "grad_sumsq")
         clip = self._sumsq.data_ptr() if self.max_grad_norm > 0 else None
         steps_ptr = self._steps_dev.data_ptr()
         if self.capturable:
             sched, nsteps = self._device_schedule(dev, self.step_count)
             L.check(lib.mdemi_adamw_step_dev(tl_ptr, nt, sched.data_ptr(), nsteps, len(self.param_groups),
-                                             self._step_dev.data_ptr(), steps_ptr, clip, self.max_grad_norm, ni,
-                                             ws_ptr, L.stream()), "adamw_step_dev")
+                                             self._step_dev.data_ptr(), steps_ptr, clip, self.max_grad_norm, gs,
+                                             ni, ws_ptr, L.stream()), "adamw_step_dev")
         else:
             groups = (L.AdamWGroup * len(self.param_groups))()
             for i, g in enumerate(self.param_groups):
                 groups[i].lr, (groups[i].beta1, groups[i].beta2) = g["lr"], g["betas"]
                 groups[i].eps, groups[i].weight_decay = g["eps"], g["weight_decay"]
-            L.check(lib.mdemi_adamw_step(tl_ptr, nt, groups, len(self.param_groups), clip, self.max_grad_norm,
+            L.check(lib.mdemi_adamw_step(tl_ptr, nt, groups, len(self.param_groups), clip, self.max_grad_norm, gs,
                                          self.step_count + 1, steps_ptr, ni, ws_ptr, L.stream()), "adamw_step")
         if not capturing:  # a capture records the step; replays advance the mirrors (replayed())
             self.replayed()

@@ -8,6 +8,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import bf16emu as E
 from . import bnmode
 
 
@@ -16,7 +17,7 @@ def ln(P, pre, x, eps=1e-5):
 
 
 def lin(P, pre, x):
-    return F.linear(x, P[pre + "weight"], P[pre + "bias"])
+    return E.linear(x, P[pre + "weight"], P[pre + "bias"])
 
 
 def conv_bn(P, pre, x, act=True, use_residual=True):  # layer_utils.py:6-34
@@ -25,7 +26,7 @@ def conv_bn(P, pre, x, act=True, use_residual=True):  # layer_utils.py:6-34
     identity = x
     if k > 1:
         x = F.pad(x, (k // 2, k // 2, k // 2, k // 2), mode="replicate")
-    x = F.conv2d(x, w)
+    x = E.conv2d(x, w)
     x = bnmode.batch_norm(P, pre + "bn.", x, 1e-5)
     if act:
         x = F.silu(x)
@@ -61,18 +62,18 @@ def prenorm_luna_block(P, pre, hidden, aux, heads):  # luna_layer.py:181-259
     q1 = _split_heads(lin(P, pre + "q1_proj.", aux_n), heads)
     k1 = _split_heads(lin(P, pre + "k1_proj.", hidden_n), heads)
     v1 = _split_heads(lin(P, pre + "v1_proj.", hidden_n), heads)
-    attn1 = torch.matmul(q1, k1.transpose(-2, -1))
+    attn1 = E.matmul(q1, k1.transpose(-2, -1))
     attn1 = torch.softmax(attn1 * scale, dim=-1)
-    out1 = torch.matmul(attn1, v1).transpose(1, 2).reshape(b, -1, d)
+    out1 = E.matmul(attn1, v1).transpose(1, 2).reshape(b, -1, d)
     out1 = lin(P, pre + "o1_proj.", out1)
     aux_out = aux + out1
     out_n = ln(P, pre + "inter_norm.", out1)
     q2 = _split_heads(lin(P, pre + "q2_proj.", hidden_n), heads)
     k2 = _split_heads(lin(P, pre + "k2_proj.", out_n), heads)
     v2 = _split_heads(lin(P, pre + "v2_proj.", out_n), heads)
-    attn2 = torch.matmul(q2, k2.transpose(-2, -1))
+    attn2 = E.matmul(q2, k2.transpose(-2, -1))
     attn2 = torch.softmax(attn2 * scale, dim=-1)
-    out2 = torch.matmul(attn2, v2).transpose(1, 2).reshape(b, -1, d)
+    out2 = E.matmul(attn2, v2).transpose(1, 2).reshape(b, -1, d)
     out2 = lin(P, pre + "o2_proj.", out2)
     return hidden + out2, aux_out, attn1, attn2
 
@@ -99,8 +100,8 @@ def self_attention_block(P, pre, hidden, heads):  # self_attention.py:44-88
     k = _split_heads(lin(P, pre + "key_proj.", h), heads)
     v = _split_heads(lin(P, pre + "value_proj.", h), heads)
     scale = math.sqrt(1.0 / q.shape[-1])
-    attn = torch.softmax(torch.matmul(q, k.transpose(-2, -1)) * scale, dim=-1)
-    o = torch.matmul(attn, v).transpose(1, 2).reshape(b, s, -1)
+    attn = torch.softmax(E.matmul(q, k.transpose(-2, -1)) * scale, dim=-1)
+    o = E.matmul(attn, v).transpose(1, 2).reshape(b, s, -1)
     return lin(P, pre + "out_proj.", o) + residual, attn
 
 
@@ -129,7 +130,7 @@ def decoder_v8(P, pre, feats, hidden_dim, num_heads, num_aux):  # decoder_v8.py:
     out = torch.cat([out0] + up, dim=1)
     z = conv_bn(P, pre + "bin_predictor.0.", out, use_residual=False)
     z = conv_bn(P, pre + "bin_predictor.1.", z, use_residual=False)
-    bin_cls = torch.softmax(F.conv2d(z, P[pre + "bin_predictor.2.weight"], P[pre + "bin_predictor.2.bias"]), dim=1)
+    bin_cls = torch.softmax(E.conv2d(z, P[pre + "bin_predictor.2.weight"], P[pre + "bin_predictor.2.bias"]), dim=1)
     a = torch.mean(aux, dim=1)
     a = F.silu(lin(P, pre + "bin_regressor.0.", a))
     a = F.silu(lin(P, pre + "bin_regressor.3.", a))

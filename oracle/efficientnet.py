@@ -17,6 +17,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import bf16emu as E
 from . import bnmode
 
 BN_EPS = 1e-3
@@ -33,7 +34,7 @@ def conv_same(x, w, stride=1, groups=1, b=None):
     pw = max((math.ceil(iw / stride) - 1) * stride + k - iw, 0)
     if ph or pw:
         x = F.pad(x, [pw // 2, pw - pw // 2, ph // 2, ph - ph // 2])
-    return F.conv2d(x, w, b, stride=stride, groups=groups)
+    return E.conv2d(x, w, b, stride=stride, groups=groups)
 
 
 def bn(P, pre, x):
@@ -51,16 +52,16 @@ def ds_block(P, pre, x, stride, residual):
     w = P[pre + "conv_dw.weight"]
     y = F.silu(bn(P, pre + "bn1.", conv_same(x, w, stride, groups=w.shape[0])))
     y = se(P, pre + "se.", y)
-    y = bn(P, pre + "bn2.", F.conv2d(y, P[pre + "conv_pw.weight"]))
+    y = bn(P, pre + "bn2.", E.conv2d(y, P[pre + "conv_pw.weight"]))
     return y + x if residual else y
 
 
 def ir_block(P, pre, x, stride, residual):
-    y = F.silu(bn(P, pre + "bn1.", F.conv2d(x, P[pre + "conv_pw.weight"])))
+    y = F.silu(bn(P, pre + "bn1.", E.conv2d(x, P[pre + "conv_pw.weight"])))
     w = P[pre + "conv_dw.weight"]
     y = F.silu(bn(P, pre + "bn2.", conv_same(y, w, stride, groups=w.shape[0])))
     y = se(P, pre + "se.", y)
-    y = bn(P, pre + "bn3.", F.conv2d(y, P[pre + "conv_pwl.weight"]))
+    y = bn(P, pre + "bn3.", E.conv2d(y, P[pre + "conv_pwl.weight"]))
     return y + x if residual else y
 
 
@@ -85,5 +86,5 @@ def features(P, pre, x, last=11, depth_multiplier=2.2):
         if len(feats) > last:
             return feats
     if pre + "conv_head.weight" in P:
-        feats.append(F.conv2d(y, P[pre + "conv_head.weight"]))
+        feats.append(E.conv2d(y, P[pre + "conv_head.weight"]))
     return feats[:last + 1]

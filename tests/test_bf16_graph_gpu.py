@@ -9,6 +9,7 @@
 * A captured train step replays bit-for-bit what the eager step computes (dropout off),
   and with dropout on every replay draws new masks."""
 import copy
+import os
 
 import pytest
 import torch
@@ -24,6 +25,9 @@ ACC_RTOL = 2e-6
 # (measured: outputs <= 1e-3, gradients <= 7e-2 -- BatchNorm affine gradients, sums of
 # dY x-hat over every pixel, carry the largest bf16 error)
 BF16_OUT_L2, BF16_GRAD_L2 = 1e-2, 1e-1
+# GPU bf16 vs the bf16-emulating fp64 oracle, per parameter gradient, beyond 20x the CPU fp32
+# emulation's own relative L2 error (test_depthformer_v8_480x640_bf16_vs_fp64_oracle)
+BF16_EMU_GRAD_L2 = 1e-2
 
 
 @pytest.fixture(scope="module")
@@ -213,16 +217,31 @@ def test_graph_replays_draw_new_dropout_masks(mf):
 def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
     """BASELINE configs[4] at its own size: Depthformer v8 with the benchmark's decoder (hidden
     256, 4 heads, 256 bins, 256 aux tokens) at NYU 480x640, batch 2, train mode, under bf16
-    matmuls, against the fp64 oracle (oracle.depthformer, pinned to the reference by
-    tests/golden/depthformer_v8.npz; restated B5 encoder): depth, centres, the 8 attention
-    maps and EVERY parameter gradient, each within the relative-L2 bounds above
-    (BF16_OUT_L2 outputs, BF16_GRAD_L2 gradients; vanishing gradients held against a floor of
-    1e-2 x the largest gradient norm, as in the golden case).  depthformer_v8.py:46-75,
-    decoder_v8.py:97-171."""
-    import numpy as np
+    matmuls, against the oracle (oracle.depthformer, pinned to the reference by
+    tests/golden/depthformer_v8.npz; restated B5 encoder) run with the SAME bf16 numerics
+    (oracle.bf16emu: every conv / linear / matmul operand rounded to bf16, forward and
+    backward, as mdemi_gemm_bf16 does).  o64 / o32 are that bf16-operand computation carried
+    out in fp64 / fp32 on the CPU.
 
+    Outputs (depth, centres, the 8 attention maps):
+        max|gpu - o64| <= 20 x max|o32 - o64| + 1e-3 x max|o64|
+    (the fp32 full-size test's criterion).  EVERY parameter gradient, in relative L2:
+        ||gpu - o64|| / ||o64|| <= 20 x ||o32 - o64|| / ||o64|| + BF16_EMU_GRAD_L2
+    Relative L2, because bf16 rounding is discontinuous: an fp32-level difference upstream
+    moves an operand across a rounding boundary, and the gradients that are sums with heavy
+    cancellation -- the LayerNorm and projection biases feeding attention keys and queries,
+    whose exact gradients softmax's shift invariance makes (nearly) zero -- then differ by
+    more than their own size for the CPU's fp32 run as much as for the GPU's (measured:
+    luna_layers.3.luna_attn.norm.bias relative L2 15.6 GPU, 37.7 CPU fp32; gpurun log
+    profiles/round4/bf16_configs4_grad_diag.txt), while a wrong or missing term on a
+    well-conditioned gradient (o32 within ~1e-6 of o64) fails the bound.
+
+    What bf16 itself costs against the fp32 model is reported beside it: depth and centres
+    are held to BF16_OUT_L2 relative L2 against the un-rounded fp64 oracle.
+    depthformer_v8.py:46-75, decoder_v8.py:97-171."""
     import test_models_gpu as tm
     from mdemi.model.Depthformer import DepthformerV8
+    from oracle import bf16emu
     from oracle import depthformer as odf
     from oracle.weights import rng_array
 
@@ -238,34 +257,98 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
         dy = torch.from_numpy(rng_array(tuple(depth.shape), 85))
         (depth * dy.float().to(DEV)).sum().backward()
     torch.cuda.synchronize()
-    P = {k: (v.detach().double().clone().requires_grad_(True) if torch.is_floating_point(v) else v)
-         for k, v in sd.items()}
-    dr, cr, ar = odf.depthformer_v8_full(P, img.double(), opt, 1e-3, 10.0)
-    (dr * dy.double()).sum().backward()
+    gpu_out = [depth, centers] + list(attn)
+    names = ["depth", "centers"] + [f"attn{k}" for k in range(8)]
 
-    def rel_l2(a, r):
-        a, r = a.detach().double().cpu().reshape(-1), r.detach().double().reshape(-1)
-        return (torch.linalg.norm(a - r) / (torch.linalg.norm(r) + 1e-300)).item(), torch.linalg.norm(r).item()
+    def oracle(dtype, emulate):
+        P = {k: (v.detach().to(dtype).clone().requires_grad_(True) if torch.is_floating_point(v) else v)
+             for k, v in sd.items()}
+        ctx = bf16emu.enabled() if emulate else torch.no_grad()
+        with ctx:
+            d, c, a = odf.depthformer_v8_full(P, img.to(dtype), opt, 1e-3, 10.0)
+            if emulate:
+                (d * dy.to(dtype)).sum().backward()
+        return [t.detach() for t in [d, c] + list(a)], P
 
-    outs = {"depth": rel_l2(depth, dr)[0], "centers": rel_l2(centers, cr)[0]}
-    for k, (a, r) in enumerate(zip(attn, ar)):
-        outs[f"attn{k}"] = rel_l2(a, r)[0]
-    grads, norms, n = {}, {}, 0
+    o64, P64 = oracle(torch.float64, True)
+    o32, P32 = oracle(torch.float32, True)
+    plain, _ = oracle(torch.float64, False)
+
+    def within(name, got, r64, r32):
+        e_gpu = (got.detach().double().cpu() - r64).abs().max().item()
+        e_cpu = (r32.double() - r64).abs().max().item()
+        mag = r64.abs().max().item()
+        assert e_gpu <= 20.0 * e_cpu + 1e-3 * mag + 1e-12, (name, e_gpu, e_cpu, mag)
+        return e_gpu / (mag + 1e-300)
+
+    worst = []
+    for k, g, r64, r32 in zip(names, gpu_out, o64, o32):
+        worst.append((within(k, g, r64, r32), k))
+    n, diag = 0, []
     for k, p in m.named_parameters():
-        r = P[k].grad
+        r64, r32 = P64[k].grad, P32[k].grad
         n += 1
-        if r is None:
+        if r64 is None:
             assert p.grad is None or p.grad.abs().max().item() == 0, k
             continue
-        grads[k], norms[k] = rel_l2(p.grad, r)
-        norms[k] /= np.sqrt(r.numel())
+        g = p.grad.detach().double().cpu()
+        l2 = lambda a: torch.linalg.norm(a).item()  # noqa: E731
+        diag.append((l2(g - r64) / (l2(r64) + 1e-300), l2(r32.double() - r64) / (l2(r64) + 1e-300),
+                     l2(r64) / r64.numel() ** 0.5, k))
     assert n == len(list(m.parameters()))
-    floor = max(norms.values()) * 1e-2
-    for k in grads:
-        if norms[k] < floor:
-            grads[k] = grads[k] * norms[k] / floor
-    worst_out = max((e, k) for k, e in outs.items())
-    top = sorted(((e, k) for k, e in grads.items()), reverse=True)[:5]
-    print(f"configs[4] bf16 vs fp64: outputs {sorted(outs.items())}, worst gradients {top}")
-    assert worst_out[0] <= BF16_OUT_L2, worst_out
-    assert top[0][0] <= BF16_GRAD_L2, top
+    for d in sorted(diag, reverse=True)[:12]:
+        print(f"  grad rel-L2 gpu {d[0]:.3e}  cpu32 {d[1]:.3e}  rms {d[2]:.3e}  {d[3]}")
+    for e_gpu, e_cpu, _, k in diag:
+        assert e_gpu <= 20.0 * e_cpu + BF16_EMU_GRAD_L2, (k, e_gpu, e_cpu)
+
+    def rel_l2(a, r):
+        a, r = a.detach().double().cpu().reshape(-1), r.reshape(-1)
+        return (torch.linalg.norm(a - r) / torch.linalg.norm(r)).item()
+
+    cost = {k: rel_l2(g, r) for k, g, r in zip(names, gpu_out, plain)}
+    print(f"configs[4] bf16: worst max-error / magnitude vs the bf16-emulating fp64 oracle "
+          f"{sorted(worst, reverse=True)[:5]}; relative L2 vs the fp32-numerics fp64 oracle {cost}")
+    assert cost["depth"] <= BF16_OUT_L2 and cost["centers"] <= BF16_OUT_L2, cost
+
+
+def test_bf16_variants_bit_identical(mf):
+    """Every variant of the 16-bit family under bf16 -- fp32 LDS images rounded at fragment
+    read (0, 1, 2) and bf16 LDS images rounded as they are staged (3, 4; 128- / 256-row
+    tiles) -- multiplies the same bf16 values in the same MFMA positions: Linear forward /
+    dgrad / wgrad (+ bias row sums, split K) and implicit-GEMM conv forward / dgrad / wgrad
+    agree bit for bit; under fp32e the bf16-image variants fall back to variant 0."""
+    from mdemi import _lib as L
+    lib = L.load()
+    torch.manual_seed(6)
+    x0 = torch.randn(3000, 640, device=DEV)
+    w0 = torch.randn(384, 640, device=DEV) * 0.05
+    b0 = torch.randn(384, device=DEV)
+    dy = torch.randn(3000, 384, device=DEV)
+    c0 = torch.randn(2, 37, 45, 64, device=DEV)
+    cw0 = torch.randn(96, 64, 3, 3, device=DEV) * 0.05
+    outs = []
+    try:
+        for v in (0, 1, 2, 3, 4):
+            assert lib.mdemi_gemm_set_variant_m16(v) == 0
+            x, w, b = (t.clone().requires_grad_() for t in (x0, w0, b0))
+            c, cw = c0.clone().requires_grad_(), cw0.clone().requires_grad_()
+            with mf.matmul_precision("bf16"):
+                y = mf.linear(x, w, b)
+                y.backward(dy)
+                z = mf.conv2d_nhwc(c, cw, None, stride=1, pad=1)
+                z.backward(torch.ones_like(z))
+            outs.append([t.detach().clone() for t in (y, x.grad, w.grad, b.grad, z, c.grad, cw.grad)])
+        assert lib.mdemi_gemm_set_variant_m16(3) == 0
+        with mf.matmul_precision("fp32e"):
+            e3 = mf.linear(x0, w0)
+        assert lib.mdemi_gemm_set_variant_m16(0) == 0
+        with mf.matmul_precision("fp32e"):
+            e0 = mf.linear(x0, w0)
+    finally:
+        lib.mdemi_gemm_set_variant_m16(-1)
+    torch.cuda.synchronize()
+    names = ("linear fwd", "dgrad", "wgrad", "bias grad", "conv fwd", "conv dgrad", "conv wgrad")
+    for v, o in zip((1, 2, 3, 4), outs[1:]):
+        for n, a, r in zip(names, o, outs[0]):
+            assert torch.equal(a, r), f"variant {v}: {n} differs bitwise"
+    assert torch.equal(e3, e0)

@@ -101,3 +101,40 @@ def test_grad_allreduce_gpu_gradients_two_ranks():
         err = (got.double() - want).abs().max().item()
         scale = want.abs().max().item()
         assert err <= 1e-4 * scale + 1e-9, (i, err, scale)
+
+
+@pytest.mark.parametrize("capturable", [False, True])
+def test_world_scale_folded_into_adamw_is_exact(capturable):
+    """Trainer folds the data-parallel mean's 1/world into the AdamW step (FusedAdamW.grad_scale,
+    GradAllReduce.scale_in_finish = False) instead of sweeping the reduced gradients: taking
+    the gradient sums at grad_scale = 1/world -- in the clip norm and in the update -- must give
+    the parameters and moments that scaling the sums first (the libmdemi sweep finish() runs)
+    gives, bit for bit, over three clipped steps."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "monocular-depth-estimation_amd"))
+    from mdemi import _lib as L
+    from mdemi.train import FusedAdamW
+    world = 4
+    g = torch.Generator().manual_seed(7)
+    shapes = [(300, 17), (64,), (1000,), (3, 5, 7)]
+    p0 = [torch.randn(s, generator=g).cuda() for s in shapes]
+    sums = [[torch.randn(s, generator=g).cuda() * 3.0 for s in shapes] for _ in range(3)]
+    pa = [torch.nn.Parameter(t.clone()) for t in p0]
+    pb = [torch.nn.Parameter(t.clone()) for t in p0]
+    oa = FusedAdamW(pa, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5, capturable=capturable)
+    ob = FusedAdamW(pb, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5, capturable=capturable)
+    ob.grad_scale = 1.0 / world
+    for step in sums:
+        for p, s in zip(pa, step):
+            p.grad = torch.empty_like(s)
+            L.call("mdemi_elementwise", L.EW_AXPBY, s.data_ptr(), s.data_ptr(), p.grad.data_ptr(), s.numel(),
+                   1.0 / world, 0.0, L.stream())
+        for p, s in zip(pb, step):
+            p.grad = s.clone()
+        oa.step()
+        ob.step()
+    torch.cuda.synchronize()
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(oa.state[a][k], ob.state[b][k])

@@ -654,32 +654,43 @@ def _tail_plan_m_split(M, N, K, cus):
 def test_gemm_inline_combine_matches_reduce_kernel(mf, layouts):
     """Split-K slabs combined by the last-arriving piece of each tile (in split order) equal
     the separate gemm_splitk_reduce launch bit for bit, and repeated launches reuse the
-    self-resetting tile counters."""
+    self-resetting tile counters.  wgrad: the bias-gradient row sums of the pieces are
+    summed by the last arrivers too (no reduce launch), bit for bit as the reduce kernel
+    sums them; with and without the fused bias epilogue (16-B epilogue and per-element
+    path: N = 300 and N = 298)."""
     from mdemi import _lib as L
     lib = L.load()
-    M, N, K = 700, 300, 5000
-    a = torch.randn(M, K, device=DEV)
-    b = torch.randn(N, K, device=DEV)
-    at, bt = a.t().contiguous(), b.t().contiguous()
+    for M, N, K in ((700, 300, 5000), (700, 298, 5000)):
+        a = torch.randn(M, K, device=DEV)
+        b = torch.randn(N, K, device=DEV)
+        bias = torch.randn(N, device=DEV)
+        at, bt = a.t().contiguous(), b.t().contiguous()
 
-    def run(inline):
-        L.check(lib.mdemi_gemm_set_options(1, inline), "set_options")
-        c = torch.empty(M, N, device=DEV)
-        if layouts == "fwd":
-            mf.gemm(a, b, c, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG, split_k=6)
-        else:
-            mf.gemm(at, bt, c, M, N, K, lda=M, ldb=N, ldc=N, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
-                    split_k=6)
-        return c
+        def run(inline):
+            L.check(lib.mdemi_gemm_set_options(1, inline), "set_options")
+            c = torch.empty(M, N, device=DEV)
+            rs = None
+            if layouts == "fwd":
+                mf.gemm(a, b, c, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG, split_k=6,
+                        bias=bias, bias_mode=L.BIAS_COL)
+            else:
+                rs = torch.empty(M, device=DEV)
+                mf.gemm(at, bt, c, M, N, K, lda=M, ldb=N, ldc=N, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+                        split_k=6, rowsum_a=rs)
+            return c, rs
 
-    try:
-        k = run(0)
-        outs = [run(1) for _ in range(3)]
-    finally:
-        lib.mdemi_gemm_set_options(1, 1)
-    close(k, (a.double() @ b.double().t()).float(), rtol=1e-5 * math.sqrt(K))
-    for c in outs:
-        assert torch.equal(c, k)
+        try:
+            k, krs = run(0)
+            outs = [run(1) for _ in range(3)]
+        finally:
+            lib.mdemi_gemm_set_options(1, 1)
+        want = a.double() @ b.double().t() + (bias.double() if layouts == "fwd" else 0.0)
+        close(k, want.float(), rtol=1e-5 * math.sqrt(K))
+        for c, rs in outs:
+            assert torch.equal(c, k)
+            if rs is not None:
+                close(rs, a.double().sum(1).float(), rtol=1e-5 * math.sqrt(K))
+                assert torch.equal(rs, krs)
 
 
 def test_linear_and_mlp_drop_scale(mf):

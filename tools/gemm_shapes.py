@@ -15,13 +15,23 @@ from mdemi import functional as mf  # noqa: E402
 
 
 def main():
+    import copy
+
+    from mdemi.train import build_from_config
     args = bench.parse()
     dev = torch.device("cuda", 0)
-    cfg = bench.WORKLOADS[args.model]
-    model, opt, loss_fn = bench.build(args, dev)
-    img, gt = bench.synthetic_batch(cfg["batch"], cfg["h"], cfg["w"], dev, seed=1)
+    wl = bench.WORKLOADS[args.model]
+    opt = copy.deepcopy(wl["opt"])
+    B = args.batch or int(opt["dataloader"]["batch_size"])
+    opt["dataloader"]["batch_size"] = B
+    H, W = args.height or wl["h"], args.width or wl["w"]
+    precision = args.precision or wl.get("precision", "fp32")
+    torch.manual_seed(0)
+    trainer = build_from_config(opt, device=dev, precision=precision)
+    batches = [bench.synthetic_batch(B, H, W, dev, seed=1000 + i, data_type=opt["dataset"]["data_type"])
+               for i in range(trainer.num_accum)]
     for _ in range(2):
-        bench.train_step(model, opt, loss_fn, img, gt)
+        trainer.step(batches)
     torch.cuda.synchronize()
     recs = []
     orig = mf.gemm
@@ -40,7 +50,7 @@ def main():
 
     mf.gemm = timed
     try:
-        bench.train_step(model, opt, loss_fn, img, gt)
+        trainer.step(batches)
         torch.cuda.synchronize()
     finally:
         mf.gemm = orig
