@@ -342,8 +342,8 @@ def roofline_entry(trainer, batches, workload_key, ms):
     (al, bl, aop, bop), (fl, t, cnt, alg) = dom
     ach = fl / t / 1e12
     prec = trainer.precision
-    if prec == "fp32":
-        kname, peak, regex = "gemm_f32_kernel", FP32_MFMA_PEAK_TFLOPS, f"gemm_f32_kernel<{al}, {bl}, {aop}, {bop},"
+    if prec == "fp32":  # register-staged gemm_f32_kernel and direct-to-LDS gemm_glds_kernel: one family
+        kname, peak, regex = "gemm_f32_kernel|gemm_glds_kernel", FP32_MFMA_PEAK_TFLOPS, f"gemm_f32<{al}, {bl}, {aop}, {bop}>"
     else:  # the 16-bit family: NP = 1 (bf16) or 3 (fp32e) planes
         np_ = 1 if prec == "bf16" else 3
         kname = "gemm_m16_kernel"

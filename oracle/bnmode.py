@@ -26,6 +26,7 @@ def eval_bn():
 def batch_norm(P, pre, x, eps):
     """pre: the module prefix ending in '.' (weight, bias, running_mean, running_var)."""
     if EVAL:
-        return F.batch_norm(x, P[pre + "running_mean"], P[pre + "running_var"], P[pre + "weight"], P[pre + "bias"],
-                            training=False, eps=eps)
+        # running statistics are buffers, never differentiated (a caller may hand them over as leaves)
+        return F.batch_norm(x, P[pre + "running_mean"].detach(), P[pre + "running_var"].detach(), P[pre + "weight"],
+                            P[pre + "bias"], training=False, eps=eps)
     return F.batch_norm(x, None, None, P[pre + "weight"], P[pre + "bias"], training=True, eps=eps)

@@ -10,6 +10,7 @@
   and with dropout on every replay draws new masks."""
 import copy
 import os
+import re
 
 import pytest
 import torch
@@ -28,6 +29,7 @@ BF16_OUT_L2, BF16_GRAD_L2 = 1e-2, 1e-1
 # GPU bf16 vs the bf16-emulating fp64 oracle, per parameter gradient, beyond 20x the CPU fp32
 # emulation's own relative L2 error (test_depthformer_v8_480x640_bf16_vs_fp64_oracle)
 BF16_EMU_GRAD_L2 = 1e-2
+BF16_VANISHING = re.compile(r"(k1_proj|k2_proj|key_proj)\.bias$|luna_attn\.norm\.bias$")
 
 
 @pytest.fixture(scope="module")
@@ -214,7 +216,8 @@ def test_graph_replays_draw_new_dropout_masks(mf):
     assert len(set(losses[2:])) == 3
 
 
-def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
+@pytest.mark.parametrize("bn", ["train", "eval"])
+def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf, bn):
     """BASELINE configs[4] at its own size: Depthformer v8 with the benchmark's decoder (hidden
     256, 4 heads, 256 bins, 256 aux tokens) at NYU 480x640, batch 2, train mode, under bf16
     matmuls, against the oracle (oracle.depthformer, pinned to the reference by
@@ -241,7 +244,9 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
     depthformer_v8.py:46-75, decoder_v8.py:97-171."""
     import test_models_gpu as tm
     from mdemi.model.Depthformer import DepthformerV8
-    from oracle import bf16emu
+    import contextlib
+
+    from oracle import bf16emu, bnmode
     from oracle import depthformer as odf
     from oracle.weights import rng_array
 
@@ -251,6 +256,10 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
     m = DepthformerV8.build(opt, 1e-3, 10.0)
     sd = tm._filled_state(m, 0.53, 0.03)
     m = m.to(DEV).train()
+    if bn == "eval":  # BatchNorm on running statistics (everything else in train mode)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.eval()
     img = torch.from_numpy(rng_array((2, 3, 480, 640), 84))
     with mf.matmul_precision("bf16"):
         depth, centers, attn = m(img.float().to(DEV))
@@ -264,7 +273,7 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
         P = {k: (v.detach().to(dtype).clone().requires_grad_(True) if torch.is_floating_point(v) else v)
              for k, v in sd.items()}
         ctx = bf16emu.enabled() if emulate else torch.no_grad()
-        with ctx:
+        with ctx, (bnmode.eval_bn() if bn == "eval" else contextlib.nullcontext()):
             d, c, a = odf.depthformer_v8_full(P, img.to(dtype), opt, 1e-3, 10.0)
             if emulate:
                 (d * dy.to(dtype)).sum().backward()
@@ -298,8 +307,17 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
     assert n == len(list(m.parameters()))
     for d in sorted(diag, reverse=True)[:12]:
         print(f"  grad rel-L2 gpu {d[0]:.3e}  cpu32 {d[1]:.3e}  rms {d[2]:.3e}  {d[3]}")
-    for e_gpu, e_cpu, _, k in diag:
-        assert e_gpu <= 20.0 * e_cpu + BF16_EMU_GRAD_L2, (k, e_gpu, e_cpu)
+    bad = [(k, e_gpu, e_cpu) for e_gpu, e_cpu, _, k in diag if e_gpu > 20.0 * e_cpu + BF16_EMU_GRAD_L2]
+    print(f"  beyond the bound: {bad}")
+    for k, e_gpu, e_cpu in bad:
+        # a gradient that softmax's shift invariance cancels to (near) zero in exact arithmetic --
+        # a bias of a key projection, or a LayerNorm bias whose only consumer is the fused
+        # key/value/query projection (luna_layer.py:202-250: colsum of dK is exactly zero) -- is
+        # bf16 rounding residue on both sides: held in size only, like the golden tests' vanishing
+        # gradients (tests/test_oda2_gpu.py VANISHING)
+        assert BF16_VANISHING.search(k), (k, e_gpu, e_cpu)
+        g = dict(m.named_parameters())[k].grad.detach().double().cpu()
+        assert torch.linalg.norm(g) <= 10.0 * torch.linalg.norm(P64[k].grad), k
 
     def rel_l2(a, r):
         a, r = a.detach().double().cpu().reshape(-1), r.reshape(-1)

@@ -10,14 +10,30 @@ timed steps count: a step ends with the single mdemi::adamw_kernel dispatch,
 so dispatches after the `warmup`-th adamw are kept (this excludes the GEMM
 autotuner's first-use timing launches).  Launches are grouped by the
 template-argument prefix `gemm_f32_kernel<A, B, AOP, BOP,` that bench.py's
-roofline names, so whichever family dominates a run finds its traffic."""
+roofline names, so whichever family dominates a run finds its traffic.  The fp32 family's
+two kernel templates -- register-staged gemm_f32_kernel<A, B, AOP, BOP, ...> and the
+direct-to-LDS gemm_glds_kernel<A, B, ...> (no load-time op) -- are one family, keyed
+`gemm_f32<A, B, AOP, BOP>`: the per-shape autotuner picks among them."""
 import csv
 import json
 import re
 import sys
 
-FAMILY = re.compile(r"gemm_f32_kernel<\d+, \d+, \d+, \d+,|gemm_m16_kernel<\d+, \d+, \d+, \d+, \d+,|"
-                    r"winattn_\w+_kernel|binhead_nhwc_\w+")
+FAMILY = re.compile(r"gemm_f32_kernel<\d+, \d+, \d+, \d+,|gemm_glds_kernel<\d+, \d+,|"
+                    r"gemm_m16_kernel<\d+, \d+, \d+, \d+, \d+,|winattn_\w+_kernel|binhead_nhwc_\w+")
+F32 = re.compile(r"gemm_f32_kernel<(\d+), (\d+), (\d+), (\d+),")
+GLDS = re.compile(r"gemm_glds_kernel<(\d+), (\d+),")
+
+
+def family_key(match):
+    """Canonical family of a kernel-name match (see the module docstring)."""
+    m = F32.match(match)
+    if m:
+        return "gemm_f32<{}, {}, {}, {}>".format(*m.groups())
+    m = GLDS.match(match)
+    if m:
+        return "gemm_f32<{}, {}, 0, 0>".format(*m.groups())
+    return match
 
 
 def per_family(path, counter, warmup):
@@ -30,7 +46,7 @@ def per_family(path, counter, warmup):
             continue
         m = FAMILY.search(name)
         if seen_adam >= warmup and m and r["Counter_Name"] == counter:
-            vals.setdefault(m.group(0), []).append(float(r["Counter_Value"]) * 1024.0)
+            vals.setdefault(family_key(m.group(0)), []).append(float(r["Counter_Value"]) * 1024.0)
     return vals
 
 
