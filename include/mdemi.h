@@ -335,6 +335,15 @@ int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y, const floa
 int mdemi_chnorm_apply(const float* x, const float* gamma, const float* beta, const float* mean,
                        const float* rstd, float* y, int32_t N, int64_t HW, int32_t C, int32_t groups,
                        int32_t is_bn, int32_t act, void* stream);
+/* backward of mdemi_chnorm_apply for BatchNorm (eval-mode BN inside a training step:
+ * frozen statistics, so dx = gamma * rstd * act'(pre) * dy with no batch terms);
+ * dx may be NULL (input needs no gradient); dgamma and dbeta are both NULL (frozen
+ * affine) or both set, and then need mdemi_chnorm_workspace_size(..., is_bn=1) bytes.
+ * Replaces autograd through F.batch_norm(training=False) where the reference trains
+ * with BatchNorm layers in eval mode (unet_adaptive_bins.py freeze, layer_utils.py). */
+int mdemi_bn_frozen_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
+                        const float* gamma, const float* beta, float* dx, float* dgamma, float* dbeta,
+                        int32_t N, int64_t HW, int32_t C, int32_t act, void* workspace, void* stream);
 /* BatchNorm2d running-statistics update in training (nn.BatchNorm2d
  * semantics: unbiased batch variance, running = (1-m) running + m batch), from
  * the batch mean / rstd of mdemi_chnorm_fwd over `rows` = N*H*W samples. One

@@ -502,6 +502,86 @@ extern "C" int mdemi_chnorm_apply(const float* x, const float* gamma, const floa
   return check_launch("chnorm_apply");
 }
 
+// Backward of the inference-mode normalisation (BatchNorm2d in eval mode inside a
+// training step, e.g. a frozen encoder's BN): mean / rstd are constants, so
+// dx = gamma * rstd * act'(pre) * dy with no batch terms; dgamma / dbeta are the same
+// channel sums as in training (bn_partial4<2> / bn_bwd_partial).
+__global__ __launch_bounds__(CN_THREADS) void bn_frozen_dx(const float* __restrict__ dy, const float* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* __restrict__ dx,
+                                                           int64_t total, int C, int act) {
+  for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total; e += (int64_t)gridDim.x * CN_THREADS) {
+    const int c = (int)(e % C);
+    const float rs = rstd[c], ga = gamma[c];
+    const float pre = (x[e] - mean[c]) * rs * ga + beta[c];
+    dx[e] = ga * rs * (dy[e] * act_grad(act, pre, apply_act(act, pre)));
+  }
+}
+
+__global__ __launch_bounds__(CN_THREADS) void bn_frozen_dx4(const float* __restrict__ dy, const float* __restrict__ x,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float* __restrict__ dx,
+                                                            int64_t total4, int CQ, int act) {
+  for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
+    const int c = 4 * (int)(e % CQ);
+    const float4 v = reinterpret_cast<const float4*>(x)[e];
+    const float4 g = reinterpret_cast<const float4*>(dy)[e];
+    const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
+    float4 o;
+#define MDEMI_BNF(X)                                                   \
+  {                                                                     \
+    const float pre = (v.X - mu.X) * rs.X * ga.X + be.X;                \
+    o.X = ga.X * rs.X * (g.X * act_grad(act, pre, apply_act(act, pre))); \
+  }
+    MDEMI_BNF(x) MDEMI_BNF(y) MDEMI_BNF(z) MDEMI_BNF(w)
+#undef MDEMI_BNF
+    reinterpret_cast<float4*>(dx)[e] = o;
+  }
+}
+
+extern "C" int mdemi_bn_frozen_bwd(const float* dy, const float* x, const float* mean, const float* rstd,
+                                   const float* gamma, const float* beta, float* dx, float* dgamma, float* dbeta,
+                                   int32_t N, int64_t HW, int32_t C, int32_t act, void* workspace, void* stream) {
+  MDEMI_REQUIRE(dy && x && mean && rstd && gamma && beta && N > 0 && HW > 0 && C > 0, "bn_frozen_bwd: bad args");
+  MDEMI_REQUIRE((dgamma == nullptr) == (dbeta == nullptr), "bn_frozen_bwd: dgamma and dbeta go together");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t rows = (int64_t)N * HW;
+  const bool vec = C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 &&
+                   (dx == nullptr || ((uintptr_t)dx & 15) == 0);
+  if (dgamma) {
+    if (!workspace) { set_error("bn_frozen_bwd: workspace required"); return MDEMI_EWORKSPACE; }
+    float* part = (float*)workspace;
+    if (vec) {
+      const int nb = bn4_blocks(rows);
+      hipLaunchKernelGGL(bn_partial4<2>, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta, part, rows,
+                         C, act, cdiv(rows, nb));
+      hipLaunchKernelGGL(bn_combine4<2>, dim3(bn4_combine_grid(C)), dim3(256), 0, st, part, nb, C, rows, 0.f, dgamma,
+                         dbeta);
+    } else {
+      const int rpb = rows_per_block(rows);
+      const int nblk = (int)cdiv(rows, rpb);
+      hipLaunchKernelGGL(bn_bwd_partial, dim3(nblk), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma, beta, part,
+                         rows, C, act, rpb);
+      hipLaunchKernelGGL(bn_bwd_combine, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, dgamma, dbeta);
+    }
+  }
+  if (dx) {
+    if (vec) {
+      const int64_t total4 = rows * C / 4;
+      hipLaunchKernelGGL(bn_frozen_dx4, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma, beta,
+                         dx, total4, C / 4, act);
+    } else {
+      hipLaunchKernelGGL(bn_frozen_dx, dim3(grid_for(rows * C)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma,
+                         beta, dx, rows * C, C, act);
+    }
+  }
+  return check_launch("bn_frozen_bwd");
+}
+
 __global__ void bn_running_kernel(const float* __restrict__ mean, const float* __restrict__ rstd,
                                   float* __restrict__ rmean, float* __restrict__ rvar, int C, float unbias, float eps,
                                   float m) {

@@ -1143,8 +1143,51 @@ def drop_path_add(res, branch, drop_prob, training):
     return _DropPathAddFn.apply(res, branch, drop_path_scale(branch.shape[0], drop_prob, branch.device))
 
 
+class _BatchNormEvalFn(torch.autograd.Function):
+    """BatchNorm2d with running statistics (eval mode), differentiable: a BN frozen by
+    freeze_bn (common_utils.py:78-81) inside a training step still passes gradients to
+    its input and its affine parameters, as F.batch_norm(training=False) does."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, act):
+        _require_cuda(x, weight, bias)
+        x = _c(x)
+        n, c = x.shape[0], x.shape[-1]
+        hw = x[0].numel() // c
+        mean = running_mean.detach().clone()  # later running-stat updates must not reach backward
+        rstd = torch.rsqrt(running_var.detach() + eps)
+        y = torch.empty_like(x)
+        L.call("mdemi_chnorm_apply", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), mean.data_ptr(),
+               rstd.data_ptr(), y.data_ptr(), n, hw, c, c, 1, act, L.stream())
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        dy = _c(dy)
+        n, c = x.shape[0], x.shape[-1]
+        hw = x[0].numel() // c
+        want_dx = ctx.needs_input_grad[0]
+        want_p = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dx = torch.empty_like(x) if want_dx else None
+        dg = torch.empty(c, device=x.device, dtype=torch.float32) if want_p else None
+        db = torch.empty(c, device=x.device, dtype=torch.float32) if want_p else None
+        lib = L.load()
+        ws = L.workspace(lib.mdemi_chnorm_workspace_size(n, hw, c, c, 1), x.device) if want_p else None
+        L.check(lib.mdemi_bn_frozen_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                        weight.data_ptr(), bias.data_ptr(), L.ptr(dx), L.ptr(dg), L.ptr(db), n, hw, c,
+                                        ctx.act, L.ptr(ws), L.stream()), "bn_frozen_bwd")
+        return (dx, dg if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None, None, None,
+                None, None)
+
+
 def batch_norm_eval_nhwc(x, weight, bias, running_mean, running_var, eps=1e-5, act=L.ACT_NONE):
-    """Inference BatchNorm2d (running statistics); no autograd."""
+    """BatchNorm2d with running statistics over an NHWC map (eval mode); differentiable
+    when a gradient is wanted, a single launch otherwise."""
+    if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad or bias.requires_grad):
+        return _BatchNormEvalFn.apply(x, weight, bias, running_mean, running_var, eps, act)
     _require_cuda(x)
     x = _c(x)
     n, c = x.shape[0], x.shape[-1]

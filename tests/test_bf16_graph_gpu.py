@@ -10,7 +10,6 @@
   and with dropout on every replay draws new masks."""
 import copy
 import os
-import re
 
 import pytest
 import torch
@@ -29,7 +28,10 @@ BF16_OUT_L2, BF16_GRAD_L2 = 1e-2, 1e-1
 # GPU bf16 vs the bf16-emulating fp64 oracle, per parameter gradient, beyond 20x the CPU fp32
 # emulation's own relative L2 error (test_depthformer_v8_480x640_bf16_vs_fp64_oracle)
 BF16_EMU_GRAD_L2 = 1e-2
-BF16_VANISHING = re.compile(r"(k1_proj|k2_proj|key_proj)\.bias$|luna_attn\.norm\.bias$")
+# a gradient whose bf16 rounding noise (bf16-emulating fp64 oracle vs the un-rounded fp64
+# oracle) is at least this fraction of its size is decided by where roundings fall, not by
+# the arithmetic: held to lie within BF16_NOISE_BALL x that noise of the emulation
+BF16_NOISE_DOMINATED, BF16_NOISE_BALL = 0.1, 2.0
 
 
 @pytest.fixture(scope="module")
@@ -231,13 +233,17 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf, bn):
     (the fp32 full-size test's criterion).  EVERY parameter gradient, in relative L2:
         ||gpu - o64|| / ||o64|| <= 20 x ||o32 - o64|| / ||o64|| + BF16_EMU_GRAD_L2
     Relative L2, because bf16 rounding is discontinuous: an fp32-level difference upstream
-    moves an operand across a rounding boundary, and the gradients that are sums with heavy
-    cancellation -- the LayerNorm and projection biases feeding attention keys and queries,
-    whose exact gradients softmax's shift invariance makes (nearly) zero -- then differ by
-    more than their own size for the CPU's fp32 run as much as for the GPU's (measured:
-    luna_layers.3.luna_attn.norm.bias relative L2 15.6 GPU, 37.7 CPU fp32; gpurun log
-    profiles/round4/bf16_configs4_grad_diag.txt), while a wrong or missing term on a
-    well-conditioned gradient (o32 within ~1e-6 of o64) fails the bound.
+    moves an operand across a rounding boundary.  Gradients that are sums with heavy
+    cancellation are bf16 rounding residue: a value-projection bias's gradient is sum_i dO_i
+    (sum_j P~_ij) with P~ the bf16-rounded probabilities whose rows no longer sum to one; a key
+    projection's bias gradient is exactly zero by softmax's shift invariance.  For those the
+    emulation itself moves the gradient by more than its size (measured on the CPU, train-mode
+    BN: luna_layers.2.luna_attn.v1_proj.bias relative L2 3.49 between the bf16-emulating and the
+    un-rounded fp64 oracle).  So the noise n = ||o64 - plain64|| / ||o64|| is measured per
+    parameter, and a gradient with n >= BF16_NOISE_DOMINATED is held to
+        ||gpu - o64|| / ||o64|| <= BF16_NOISE_BALL x n
+    (the GPU's rounding lands inside the emulation's noise ball), while every other gradient
+    -- a wrong or missing term on a well-conditioned gradient -- takes the bound above.
 
     What bf16 itself costs against the fp32 model is reported beside it: depth and centres
     are held to BF16_OUT_L2 relative L2 against the un-rounded fp64 oracle.
@@ -272,16 +278,15 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf, bn):
     def oracle(dtype, emulate):
         P = {k: (v.detach().to(dtype).clone().requires_grad_(True) if torch.is_floating_point(v) else v)
              for k, v in sd.items()}
-        ctx = bf16emu.enabled() if emulate else torch.no_grad()
+        ctx = bf16emu.enabled() if emulate else contextlib.nullcontext()
         with ctx, (bnmode.eval_bn() if bn == "eval" else contextlib.nullcontext()):
             d, c, a = odf.depthformer_v8_full(P, img.to(dtype), opt, 1e-3, 10.0)
-            if emulate:
-                (d * dy.to(dtype)).sum().backward()
+            (d * dy.to(dtype)).sum().backward()
         return [t.detach() for t in [d, c] + list(a)], P
 
     o64, P64 = oracle(torch.float64, True)
     o32, P32 = oracle(torch.float32, True)
-    plain, _ = oracle(torch.float64, False)
+    plain, Pplain = oracle(torch.float64, False)
 
     def within(name, got, r64, r32):
         e_gpu = (got.detach().double().cpu() - r64).abs().max().item()
@@ -302,22 +307,18 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf, bn):
             continue
         g = p.grad.detach().double().cpu()
         l2 = lambda a: torch.linalg.norm(a).item()  # noqa: E731
-        diag.append((l2(g - r64) / (l2(r64) + 1e-300), l2(r32.double() - r64) / (l2(r64) + 1e-300),
+        ref = l2(r64) + 1e-300
+        diag.append((l2(g - r64) / ref, l2(r32.double() - r64) / ref, l2(Pplain[k].grad - r64) / ref,
                      l2(r64) / r64.numel() ** 0.5, k))
     assert n == len(list(m.parameters()))
     for d in sorted(diag, reverse=True)[:12]:
-        print(f"  grad rel-L2 gpu {d[0]:.3e}  cpu32 {d[1]:.3e}  rms {d[2]:.3e}  {d[3]}")
-    bad = [(k, e_gpu, e_cpu) for e_gpu, e_cpu, _, k in diag if e_gpu > 20.0 * e_cpu + BF16_EMU_GRAD_L2]
-    print(f"  beyond the bound: {bad}")
-    for k, e_gpu, e_cpu in bad:
-        # a gradient that softmax's shift invariance cancels to (near) zero in exact arithmetic --
-        # a bias of a key projection, or a LayerNorm bias whose only consumer is the fused
-        # key/value/query projection (luna_layer.py:202-250: colsum of dK is exactly zero) -- is
-        # bf16 rounding residue on both sides: held in size only, like the golden tests' vanishing
-        # gradients (tests/test_oda2_gpu.py VANISHING)
-        assert BF16_VANISHING.search(k), (k, e_gpu, e_cpu)
-        g = dict(m.named_parameters())[k].grad.detach().double().cpu()
-        assert torch.linalg.norm(g) <= 10.0 * torch.linalg.norm(P64[k].grad), k
+        print(f"  grad rel-L2 gpu {d[0]:.3e}  cpu32 {d[1]:.3e}  bf16 noise {d[2]:.3e}  rms {d[3]:.3e}  {d[4]}")
+    bad = [(k, e_gpu, e_cpu, noise) for e_gpu, e_cpu, noise, _, k in diag
+           if e_gpu > 20.0 * e_cpu + BF16_EMU_GRAD_L2 and
+           not (noise >= BF16_NOISE_DOMINATED and e_gpu <= BF16_NOISE_BALL * noise)]
+    noisy = sum(1 for d in diag if d[2] >= BF16_NOISE_DOMINATED)
+    print(f"  {noisy} of {len(diag)} gradients bf16-noise-dominated; beyond the bounds: {bad}")
+    assert not bad, bad
 
     def rel_l2(a, r):
         a, r = a.detach().double().cpu().reshape(-1), r.reshape(-1)

@@ -360,6 +360,68 @@ def test_batch_norm_running_stats(mf, momentum):
     assert int(bn.num_batches_tracked) == 3
 
 
+@pytest.mark.parametrize("n,c,h,w,act,affine_grad", [(2, 48, 30, 40, 6, True), (2, 600, 9, 11, 3, True),
+                                                     (3, 6, 10, 10, 2, True), (2, 64, 7, 9, 0, False),
+                                                     (1, 5, 4, 4, 6, False)])
+def test_batch_norm_eval_backward(mf, n, c, h, w, act, affine_grad):
+    """Eval-mode BatchNorm inside a training step (freeze_bn, common_utils.py:78-81): forward
+    with the running statistics and gradients to the input and, unless frozen, the affine
+    parameters -- F.batch_norm(training=False) in fp64, through mdemi_bn_frozen_bwd (vector
+    path C % 4 == 0 and scalar path; dgamma/dbeta skipped when the affine is frozen)."""
+    from mdemi import _lib as L
+    x = rnd(n, c, h, w, seed=70, scale=3) + 1
+    g, b = rnd(c, seed=71), rnd(c, seed=72)
+    rm, rv = rnd(c, seed=73), rnd(c, seed=74).abs() + 0.5
+    dy = rnd(n, c, h, w, seed=75)
+    xr = x.clone().requires_grad_()
+    gr, br = [t.clone().requires_grad_(affine_grad) for t in (g, b)]
+    yr = F.batch_norm(xr, rm, rv, gr, br, training=False, eps=1e-3)
+    yr = {L.ACT_RELU: F.relu, L.ACT_SILU: F.silu, L.ACT_LEAKY: F.leaky_relu, L.ACT_NONE: lambda t: t}[act](yr)
+    yr.backward(dy)
+    xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV).requires_grad_()
+    gg, bg = [t.float().to(DEV).requires_grad_(affine_grad) for t in (g, b)]
+    rmg, rvg = rm.float().to(DEV), rv.float().to(DEV)
+    yg = mf.batch_norm_eval_nhwc(xg, gg, bg, rmg, rvg, 1e-3, act)
+    yg.backward(dy.permute(0, 2, 3, 1).float().to(DEV))
+    close(yg.permute(0, 3, 1, 2), yr, rtol=1e-5)
+    close(xg.grad.permute(0, 3, 1, 2), xr.grad, rtol=1e-4)
+    if affine_grad:
+        close(gg.grad, gr.grad, rtol=1e-4)
+        close(bg.grad, br.grad, rtol=1e-4)
+    else:
+        assert gg.grad is None and bg.grad is None
+    close(rmg, rm, rtol=0)  # running statistics untouched in eval mode
+    with torch.no_grad():  # no-grad path: one launch, same values
+        close(mf.batch_norm_eval_nhwc(xg.detach(), gg, bg, rmg, rvg, 1e-3, act), yg.detach(), rtol=0)
+
+
+def test_freeze_bn_train_step_reaches_encoder(mf):
+    """A training step with every BatchNorm frozen (eval mode) still gives the parameters
+    below each BN a gradient: AdaBins-style conv -> BN -> act stack, compared with torch."""
+    from mdemi.model.NewCRFs.uper_crf_head import bn_forward
+    from mdemi import _lib as L
+    torch.manual_seed(3)
+    conv = torch.nn.Conv2d(8, 16, 3, padding=1, bias=False).double()
+    bn = torch.nn.BatchNorm2d(16, eps=1e-5).double()
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+    bn.eval()
+    x = rnd(2, 8, 12, 10, seed=76)
+    F.relu(bn(conv(x))).sum().backward()
+    w = conv.weight.detach().float().to(DEV).requires_grad_()
+    bng = torch.nn.BatchNorm2d(16, eps=1e-5).to(DEV)
+    bng.load_state_dict({k: v.float() for k, v in bn.state_dict().items()})
+    bng.eval()
+    xg = x.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+    yg = mf.conv2d_nhwc(xg, w, None, stride=1, pad=1)
+    bn_forward(bng, yg, L.ACT_RELU).sum().backward()
+    assert w.grad is not None and bng.weight.grad is not None
+    close(w.grad, conv.weight.grad, rtol=1e-4)
+    close(bng.weight.grad, bn.weight.grad, rtol=1e-4)
+    assert int(bng.num_batches_tracked) == 0
+
+
 @pytest.mark.parametrize("rows,C", [(300, 64), (1000, 192), (77, 1536)])
 def test_layer_norm_skip(mf, rows, C):
     """(LN(x), x) residual pattern: z = x + LN(x) W^T; the skip gradient is summed inside the

@@ -41,7 +41,7 @@ def per_family(path, counter, warmup):
     seen_adam, vals = 0, {}
     for r in rows:
         name = r["Kernel_Name"]
-        if "adamw_kernel" in name:
+        if re.search(r"adamw(_dev)?_kernel", name):
             seen_adam += 1
             continue
         m = FAMILY.search(name)

@@ -13,7 +13,7 @@ import sys
 rows = sorted(csv.DictReader(open(f"{sys.argv[1]}/run_kernel_trace.csv")), key=lambda r: int(r["Dispatch_Id"]))
 warmup = int(sys.argv[2])
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
-adam_idx = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
+adam_idx = [i for i, r in enumerate(rows) if re.search(r"adamw(_dev)?_kernel", r["Kernel_Name"])]
 lo, hi = adam_idx[warmup - 1] + 1, adam_idx[-1] + 1
 steps = len(adam_idx) - warmup
 win = rows[lo:hi]

@@ -10,7 +10,7 @@ rows = sorted(csv.DictReader(open(f"{sys.argv[1]}/run_kernel_trace.csv")), key=l
 warmup, rx = int(sys.argv[2]), re.compile(sys.argv[3])
 adam, durs, spans = 0, [], []
 for n, r in enumerate(rows):
-    if "adamw_kernel" in r["Kernel_Name"]:
+    if re.search(r"adamw(_dev)?_kernel", r["Kernel_Name"]):
         adam += 1
         continue
     if adam >= warmup and rx.search(r["Kernel_Name"]):
