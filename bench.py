@@ -217,60 +217,50 @@ def _gemm_alg_bytes(A, B, M, N, K, kw):
 
 
 class _HbmTimers:
-    """HIP events around the memory-heavy fused ops during the instrumented step, with their
-    algorithmic bytes -> achieved GB/s against the 8 TB/s HBM peak:
+    """HIP events around the C entry points of the memory-heavy fused ops during the
+    instrumented step (the events bracket the entry's own launches on its stream, so no
+    host-side gap between kernels is counted), with their algorithmic bytes -> achieved GB/s
+    against the 8 TB/s HBM peak:
       binhead_nhwc_fwd/bwd (SURVEY §8d's HBM-bound row): fwd reads the logits and writes
         pred + the (max, sum) row stats, 4*B*HW*(K+3) B; bwd reads logits, pred, stats and
         dpred and writes dlogits, 4*B*HW*(2K+4) B;
       winattn_fwd/bwd (fused shifted-window attention): fwd reads q, k, v and
         writes out, 16*C B per token; bwd reads q, k, v, out, dout and writes dq, dk, dv,
-        32*C B per token (the window's MFMA work rides on the same pass).
-    The window covers the autograd Function (its small allocations and pad fills too)."""
+        32*C B per token (the window's MFMA work rides on the same pass).  The entry also
+        launches the small relative-position-bias expansion (and, backward, its gradient
+        scatter): a few us each, counted in the window."""
 
-    def __init__(self, mf):
-        def bh_sizes(logits):
-            b, k = logits.shape[0], logits.shape[-1]
-            return b, logits[0].numel() // k, k
+    def __init__(self, lib):
+        def wa_bytes(per_token):
+            def f(args):
+                d = args[0]._obj  # ctypes.byref(WinAttnDesc)
+                return per_token * d.heads * d.head_dim * d.B * d.H * d.W
+            return f
 
-        def bh_fwd(args, ctx):
-            b, hw, k = bh_sizes(args[0])
-            return 4.0 * b * hw * (k + 3)
-
-        def bh_bwd(args, ctx):
-            b, hw, k = bh_sizes(ctx.saved_tensors[0])
-            return 4.0 * b * hw * (2 * k + 4)
-
-        def wa_fwd(args, ctx):
-            B, H, W, _, _, _, _, C, _ = args[5]
-            return 16.0 * C * B * H * W
-
-        def wa_bwd(args, ctx):
-            B, H, W, _, _, _, _, C, _ = ctx.geom
-            return 32.0 * C * B * H * W
-
-        self.specs = [(mf._BinHeadNHWCFn, "binhead_nhwc", bh_fwd, bh_bwd),
-                      (mf._WindowAttnFn, "winattn", wa_fwd, wa_bwd)]
-        self.orig = [(cls, cls.forward, cls.backward) for cls, _, _, _ in self.specs]
-        self.recs = {}
-        for cls, name, fb, bb in self.specs:
-            self.recs[name + "_fwd"], self.recs[name + "_bwd"] = [], []
-            cls.forward = staticmethod(self._wrap(cls.forward, fb, self.recs[name + "_fwd"], fwd=True))
-            cls.backward = staticmethod(self._wrap(cls.backward, bb, self.recs[name + "_bwd"], fwd=False))
+        self.specs = {"mdemi_binhead_nhwc_fwd": ("binhead_nhwc_fwd", lambda a: 4.0 * a[4] * a[5] * (a[6] + 3)),
+                      "mdemi_binhead_nhwc_bwd": ("binhead_nhwc_bwd", lambda a: 4.0 * a[7] * a[8] * (2 * a[9] + 4)),
+                      "mdemi_winattn_fwd": ("winattn_fwd", wa_bytes(16.0)),
+                      "mdemi_winattn_bwd": ("winattn_bwd", wa_bytes(32.0))}
+        self.lib = lib
+        self.orig = {entry: getattr(lib, entry) for entry in self.specs}
+        self.recs = {name: [] for name, _ in self.specs.values()}
+        for entry, (name, nbytes) in self.specs.items():
+            setattr(lib, entry, self._wrap(self.orig[entry], nbytes, self.recs[name]))
 
     @staticmethod
-    def _wrap(fn, nbytes, recs, fwd):
-        def timed(ctx, *args):
+    def _wrap(fn, nbytes, recs):
+        def timed(*args):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(torch.cuda.current_stream())
-            out = fn(ctx, *args)
+            rc = fn(*args)
             e.record(torch.cuda.current_stream())
-            recs.append((nbytes(args, ctx), s, e))
-            return out
+            recs.append((nbytes(args), s, e))
+            return rc
         return timed
 
     def restore(self):
-        for cls, f, b in self.orig:
-            cls.forward, cls.backward = staticmethod(f), staticmethod(b)
+        for entry, fn in self.orig.items():
+            setattr(self.lib, entry, fn)
 
     def summary(self):
         out = {}
@@ -304,7 +294,8 @@ def gemm_roofline(trainer, batches):
         return out
 
     mf.gemm = timed
-    hbm = _HbmTimers(mf)
+    from mdemi import _lib as L
+    hbm = _HbmTimers(L.load())
     try:
         with mf.matmul_precision(trainer.precision):
             trainer._eager_step(batches)

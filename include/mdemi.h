@@ -346,11 +346,13 @@ int mdemi_bn_frozen_bwd(const float* dy, const float* x, const float* mean, cons
                         int32_t N, int64_t HW, int32_t C, int32_t act, void* workspace, void* stream);
 /* BatchNorm2d running-statistics update in training (nn.BatchNorm2d
  * semantics: unbiased batch variance, running = (1-m) running + m batch), from
- * the batch mean / rstd of mdemi_chnorm_fwd over `rows` = N*H*W samples. One
- * launch instead of the per-layer chain of small tensor ops
- * (uper_crf_head.py:341-348, unet_adaptive_bins.py:13,16, layer_utils.py:25). */
+ * the batch mean / rstd of mdemi_chnorm_fwd over `rows` = N*H*W samples, and
+ * num_batches_tracked += 1 when that pointer is given. One launch instead of the
+ * per-layer chain of small tensor ops (uper_crf_head.py:341-348,
+ * unet_adaptive_bins.py:13,16, layer_utils.py:25). */
 int mdemi_bn_running_update(const float* mean, const float* rstd, float* running_mean, float* running_var,
-                            int32_t C, int64_t rows, float eps, float momentum, void* stream);
+                            int64_t* num_batches_tracked, int32_t C, int64_t rows, float eps, float momentum,
+                            void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Elementwise helpers                                                       */

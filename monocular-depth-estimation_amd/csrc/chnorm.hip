@@ -409,6 +409,9 @@ extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float*
       const int nb = bn4_blocks(rows);
       const int64_t rpb4 = cdiv(rows, nb);
       const unsigned cg = bn4_combine_grid(C);
+      // two passes (mean, then the centred sum of squares): a one-pass Welford/Chan form saved
+      // a read of x but moved the statistics by rounding, enough to flip kink- and
+      // cancellation-sensitive parity tests; kept two-pass
       hipLaunchKernelGGL(bn_partial4<0>, dim3(nb), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma, beta, part,
                          rows, C, act, rpb4);
       hipLaunchKernelGGL(bn_combine4<0>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, mean, nullptr);
@@ -583,9 +586,10 @@ extern "C" int mdemi_bn_frozen_bwd(const float* dy, const float* x, const float*
 }
 
 __global__ void bn_running_kernel(const float* __restrict__ mean, const float* __restrict__ rstd,
-                                  float* __restrict__ rmean, float* __restrict__ rvar, int C, float unbias, float eps,
-                                  float m) {
+                                  float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ tracked,
+                                  int C, float unbias, float eps, float m) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tracked && c == 0) tracked[0] += 1;  // nn.BatchNorm2d.num_batches_tracked
   if (c >= C) return;
   const float r = rstd[c];
   const float var = (1.f / (r * r) - eps) * unbias;
@@ -594,10 +598,11 @@ __global__ void bn_running_kernel(const float* __restrict__ mean, const float* _
 }
 
 extern "C" int mdemi_bn_running_update(const float* mean, const float* rstd, float* running_mean, float* running_var,
-                                       int32_t C, int64_t rows, float eps, float momentum, void* stream) {
+                                       int64_t* num_batches_tracked, int32_t C, int64_t rows, float eps,
+                                       float momentum, void* stream) {
   MDEMI_REQUIRE(mean && rstd && running_mean && running_var && C > 0 && rows > 0, "bn_running_update: bad args");
   const float unbias = (float)((double)rows / (double)(rows > 1 ? rows - 1 : 1));
   hipLaunchKernelGGL(bn_running_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, mean, rstd,
-                     running_mean, running_var, C, unbias, eps, momentum);
+                     running_mean, running_var, num_batches_tracked, C, unbias, eps, momentum);
   return check_launch("bn_running_update");
 }

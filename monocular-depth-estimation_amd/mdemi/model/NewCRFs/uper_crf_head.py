@@ -55,13 +55,13 @@ def bn_forward(bn: nn.BatchNorm2d, x, act=L.ACT_NONE):
         if bn.track_running_stats:
             with torch.no_grad():
                 n = x.numel() // x.shape[-1]
-                bn.num_batches_tracked.add_(1)
                 if bn.momentum is None:  # cumulative average: needs the count on the host
-                    m = 1.0 / float(bn.num_batches_tracked)
-                else:
-                    m = bn.momentum
+                    bn.num_batches_tracked.add_(1)
+                    m, tracked = 1.0 / float(bn.num_batches_tracked), None
+                else:  # the counter rides on the update launch
+                    m, tracked = bn.momentum, bn.num_batches_tracked.data_ptr()
                 L.call("mdemi_bn_running_update", mean.data_ptr(), rstd.data_ptr(), bn.running_mean.data_ptr(),
-                       bn.running_var.data_ptr(), x.shape[-1], n, float(bn.eps), float(m), L.stream())
+                       bn.running_var.data_ptr(), tracked, x.shape[-1], n, float(bn.eps), float(m), L.stream())
         return y
     return mf.batch_norm_eval_nhwc(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, act)
 

@@ -203,11 +203,12 @@ class Trainer:
     numerics -- while master weights, optimizer state and the other kernels stay fp32.
 
     graph=True: the first two calls run eagerly (they settle GEMM autotuning, every
-    workspace, the optimizer state and, data-parallel, the RCCL communicator; gradients
-    stay allocated), the third captures the whole step -- forward, loss, backward, the
-    bucketed RCCL all-reduces the backward hooks launch, the 1/world scaling, clip, AdamW
-    with its schedule read on the device -- into a hipGraph (torch.cuda.CUDAGraph) and
-    replays it; every later call copies its batch into the static input buffers and
+    workspace, the optimizer state and, data-parallel, the RCCL communicator), the third
+    captures the whole step -- forward, loss, backward, the bucketed RCCL all-reduces the
+    backward hooks launch, clip and AdamW (1/world folded in) with its schedule read on the
+    device -- into a hipGraph (torch.cuda.CUDAGraph) and replays it.  Gradients are
+    persistent either way: DDP bucket views, or (single process) the tensors the captured
+    backward hands to each parameter, which every replay rewrites; every later call copies its batch into the static input buffers and
     replays.  Data-parallel, the hooks run once, at capture: the bucket launch order is
     recorded then and every replay issues the same collective sequence on every rank.
     Each call is exactly one optimizer step.  Dropout seeds are drawn on the GPU, so
@@ -272,7 +273,11 @@ class Trainer:
                 with mf.matmul_precision(self.precision):
                     return self._eager_step(batches)
             self._static = [(img.clone(), gt.clone()) for img, gt in batches]
-            self._zero_grad(set_to_none=False)
+            # without DDP buckets the gradients are None here: the captured backward hands
+            # each parameter the tensor its gradient kernel writes (AccumulateGrad steals it,
+            # from the graph's pool), so a replay rewrites .grad in place -- no per-parameter
+            # zero fill and accumulate-add in the graph (~1400 launches per Depthformer step)
+            self._zero_grad()
             if self.ddp is not None:
                 # no eager collective may still be listed with the process group's watchdog
                 # when the global-mode capture begins (quiesce_process_group)
@@ -280,7 +285,8 @@ class Trainer:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g), mf.matmul_precision(self.precision):
                 self._static_loss = self._body(self._static)
-                self._zero_grad(set_to_none=False)  # gradients keep their (captured) addresses
+                if self.ddp is not None:
+                    self.ddp.zero_grad()  # bucket views keep their (captured) addresses
             self._graph = g
             self._graph_layout = self.optimizer.layout_version
         else:
@@ -333,17 +339,17 @@ class Trainer:
         self.train_mode()
         return ck
 
-    def _zero_grad(self, set_to_none):
+    def _zero_grad(self):
         if self.ddp is not None:
             self.ddp.zero_grad()  # bucket views stay in place
         else:
-            self.optimizer.zero_grad(set_to_none=set_to_none)
+            self.optimizer.zero_grad(set_to_none=True)
 
     def _eager_step(self, batches):
         total = self._body(batches)
         if self.scheduler is not None:
             self.scheduler.step()
-        self._zero_grad(set_to_none=not self.graph)
+        self._zero_grad()
         return total
 
 

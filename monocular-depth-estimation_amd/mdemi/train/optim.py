@@ -154,9 +154,9 @@ class FusedAdamW:
         # persistent tensors (captured graphs, DDP bucket views) issues no host->device copy
         key = self._key(params)
         if key != self._tbl_key:
-            if capturing:
-                raise RuntimeError("FusedAdamW: the pointer table must be built before hipGraph capture "
-                                   "(run one eager step with the same gradients first)")
+            # inside a capture (gradients handed out by the captured backward) the upload is a
+            # memcpy node from the pinned host table, which stays alive with the device copy:
+            # every replay re-copies the same addresses
             refs, items_t, items_c, slots = self._refs()
             nt, ni = len(refs), len(items_t)
             raw = (L.TensorRef * nt)(*refs)
