@@ -589,6 +589,7 @@ class _LayerNormSkipFn(torch.autograd.Function):
         L.call("mdemi_layernorm_fwd", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
                mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), L.stream())
         ctx.save_for_backward(x, weight, mean, rstd)
+        ctx.set_materialize_grads(False)  # an unused output's gradient stays None (no zero fill)
         skip = x.view_as(x)
         return y, skip
 
@@ -955,10 +956,13 @@ class _ChNormFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, bias, mean, rstd)
         ctx.cfg = (groups, is_bn, act)
         ctx.mark_non_differentiable(mean, rstd)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the statistics
         return y, mean, rstd
 
     @staticmethod
     def backward(ctx, dy, _dm, _dr):
+        if dy is None:
+            return None, None, None, None, None, None, None
         x, weight, bias, mean, rstd = ctx.saved_tensors
         groups, is_bn, act = ctx.cfg
         dy = _c(dy)
@@ -1465,6 +1469,7 @@ class _BinsFn(torch.autograd.Function):
                mode, float(min_val), float(max_val), L.stream())
         ctx.save_for_backward(raw)
         ctx.cfg = (mode, min_val, max_val)
+        ctx.set_materialize_grads(False)
         return widths, edges, centers
 
     @staticmethod
@@ -1632,6 +1637,7 @@ class _AttentionFn(torch.autograd.Function):
              c_bstride=Sq * heads * dv, b_off=v_off, inner=(heads, hs, dv, dv))
         ctx.save_for_backward(qsrc, ksrc, vsrc, P)
         ctx.cfg = cfg
+        ctx.set_materialize_grads(False)  # unused probabilities: no zero fill + add of [B,h,Sq,Sk]
         return out, P
 
     @staticmethod
@@ -2136,6 +2142,7 @@ class _OrderedWindowAttnFn(torch.autograd.Function):
         ctx.save_for_backward(qkv, P, idx_win)
         ctx.cfg = cfg
         ctx.has_table = table is not None
+        ctx.set_materialize_grads(False)
         return out, P
 
     @staticmethod
