@@ -226,6 +226,9 @@ __global__ __launch_bounds__(CN_THREADS) void bn_partial4(const float* __restric
       const float4 mu = PASS ? ld4(mean + c) : f4(0.f);
       float4 rs = f4(1.f), ga = f4(1.f), be = f4(0.f);
       if (PASS == 2) { rs = ld4(rstd + c); ga = ld4(gamma + c); be = ld4(beta + c); }
+      // unrolled so several rows' loads are in flight per thread; each accumulator still
+      // takes the rows in order (bit-identical to the rolled loop)
+#pragma unroll 4
       for (int64_t r = r0 + lane_r; r < r1; r += rpt) {
         const float4 v = ld4(x + r * C + c);
         if (PASS == 0) {

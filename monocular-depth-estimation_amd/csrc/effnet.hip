@@ -361,7 +361,8 @@ __global__ __launch_bounds__(256) void spatial_partial(const float* __restrict__
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (cok) {
     const int64_t base = (int64_t)n * HW * C + (int64_t)c4 * 4;
-    for (int64_t p = p0 + ty; p < p1; p += 4) {
+#pragma unroll 4
+    for (int64_t p = p0 + ty; p < p1; p += 4) {  // unrolled: loads in flight, sums in row order
       const float4 u = *reinterpret_cast<const float4*>(a + base + p * C);
       if (b) {
         const float4 v = *reinterpret_cast<const float4*>(b + base + p * C);
@@ -389,7 +390,8 @@ __global__ __launch_bounds__(256) void spatial_final(const float* __restrict__ p
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)N * C) return;
   const int n = (int)(e / C), c = (int)(e % C);
-  double s = 0.0;  // fixed-order fp64 combine of the chunk partials
+  double s = 0.0;  // fixed-order fp64 combine of the chunk partials (unrolled: loads in flight)
+#pragma unroll 8
   for (int k = 0; k < nchunk; ++k) s += (double)part[((int64_t)n * nchunk + k) * C + c];
   out[e] = (float)(s * (double)scale);
 }
