@@ -120,13 +120,30 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* __restri
         if (wx == 0.f) continue;
         const float wgt = wy * wx;
         const float* src = dy + (((int64_t)n * ah.out + oy) * aw.out + ox) * dy_cs + cv * VEC;
+        float sv[VEC];
+        if constexpr (VEC == 4) {  // one 16-B load per tap (strides are multiples of 4 floats)
+          const float4 q = *reinterpret_cast<const float4*>(src);
+          sv[0] = q.x; sv[1] = q.y; sv[2] = q.z; sv[3] = q.w;
+        } else {
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) acc[v] = fmaf(wgt, src[v], acc[v]);
+          for (int v = 0; v < VEC; ++v) sv[v] = src[v];
+        }
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] = fmaf(wgt, sv[v], acc[v]);
       }
     }
     float* dst = dx + (((int64_t)n * ah.in + iy) * aw.in + ix) * dx_cs + cv * VEC;
+    if constexpr (VEC == 4) {
+      float4 o = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      if (accumulate) {
+        const float4 d = *reinterpret_cast<const float4*>(dst);
+        o.x += d.x; o.y += d.y; o.z += d.z; o.w += d.w;
+      }
+      *reinterpret_cast<float4*>(dst) = o;
+    } else {
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) dst[v] = accumulate ? dst[v] + acc[v] : acc[v];
+      for (int v = 0; v < VEC; ++v) dst[v] = accumulate ? dst[v] + acc[v] : acc[v];
+    }
   }
 }
 
@@ -265,7 +282,8 @@ extern "C" int mdemi_bilinear_bwd(const float* dout, float* dx, int32_t N, int32
   if (dx_cstride <= 0) dx_cstride = C;
   const Axis ah = make_axis(H, OH, align_corners, scale_h), aw = make_axis(W, OW, align_corners, scale_w);
   hipStream_t st = (hipStream_t)stream;
-  const bool v4 = C % 4 == 0 && dout_cstride % 4 == 0 && dx_cstride % 4 == 0;
+  const bool v4 = C % 4 == 0 && dout_cstride % 4 == 0 && dx_cstride % 4 == 0 && ((uintptr_t)dout & 15) == 0 &&
+                  ((uintptr_t)dx & 15) == 0;
   const int64_t total = (int64_t)N * H * W * (v4 ? C / 4 : C);
   if (v4)
     hipLaunchKernelGGL(bilinear_bwd_kernel<4>, dim3(grid_for(total)), dim3(256), 0, st, dout, dx, N, C, ah, aw,
