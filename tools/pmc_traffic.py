@@ -68,6 +68,8 @@ def main():
         prof = {}
     old = prof.get(workload, {}).get("families", {})
     old.update(fams)
+    for k in [k for k in old if k.startswith("gemm_f32_kernel<")]:
+        del old[k]  # pre-round-4 key form, superseded by the gemm_f32<...> family keys
     prof[workload] = {"families": old,
                       "correction": "FETCH_SIZE x2 (gfx950 half-count of 16-B coalesced reads); KB->bytes x1024",
                       "source": note}

@@ -7,7 +7,7 @@ set -e
 TAG=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 KRE=${KREGEX:-'gemm_f32_kernel|gemm_glds_kernel|adamw_kernel'}
-B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline $*"
+B="python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o run --output-format csv -- $B > gpurun_out/${TAG}_trace.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -d gpurun_out/${TAG}_fetch -o run --output-format csv -- $B > gpurun_out/${TAG}_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -d gpurun_out/${TAG}_write -o run --output-format csv -- $B > gpurun_out/${TAG}_write.log 2>&1
