@@ -39,16 +39,22 @@ def _target_blocks():
 def _split_for(M, N, K):
     """Split-K factor so that a long reduction still fills the chip.  Skinny outputs (fewer
     than 8 tiles: the weight gradients of narrow 1x1 convs over ~10^6 pixels) split up to 512
-    ways (each split still >= 256 rows of K); their slabs are combined by a column sum."""
+    ways; their slabs are combined by a column sum."""
     tiles = math.ceil(M / 128) * math.ceil(N / 128)
     ktiles = math.ceil(K / 16)
     # tools/gemm_split_study.py (profiles/r02_split_study.log): >= 384 output tiles already
-    # fill the chip (a split only adds slab traffic); each split keeps >= 512 rows of K
-    if tiles >= 384 or ktiles < 32:
+    # fill the chip (a split only adds slab traffic); each split keeps >= 256 rows of K (512
+    # until round 4: 256 takes the bf16 Depthformer step 78.95 -> 77.44 ms, NeW-CRFs
+    # unchanged, 128 slower again -- tools/gpu_r4r.sh, profiles/round4/ab_split_min_rows.txt)
+    min_kt = _SPLIT_MIN_KTILES
+    if tiles >= 384 or ktiles < min_kt:
         return 1
     target, cap = (_target_blocks(), 128) if tiles >= 8 else (2 * _target_blocks(), 512)
-    split = min(max(1, target // tiles), ktiles // 32, cap)
+    split = min(max(1, target // tiles), ktiles // min_kt, cap)
     return max(1, split)
+
+
+_SPLIT_MIN_KTILES = int(os.environ.get("MDEMI_SPLIT_MIN_KTILES", "16"))  # K tiles of 16 rows
 
 
 def _draw_seed(device):
