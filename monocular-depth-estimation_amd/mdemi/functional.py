@@ -33,7 +33,10 @@ def _c(t):
 
 
 def _target_blocks():
-    return 1024
+    return _SPLIT_TARGET_BLOCKS
+
+
+_SPLIT_TARGET_BLOCKS = int(os.environ.get("MDEMI_SPLIT_TARGET_BLOCKS", "1024"))
 
 
 def _split_for(M, N, K):
@@ -43,10 +46,11 @@ def _split_for(M, N, K):
     tiles = math.ceil(M / 128) * math.ceil(N / 128)
     ktiles = math.ceil(K / 16)
     # tools/gemm_split_study.py (profiles/r02_split_study.log): >= 384 output tiles already
-    # fill the chip (a split only adds slab traffic); each split keeps >= 256 rows of K (512
-    # until round 4: 256 takes the bf16 Depthformer step 78.95 -> 77.44 ms, NeW-CRFs
-    # unchanged, 128 slower again -- tools/gpu_r4r.sh, profiles/round4/ab_split_min_rows.txt)
-    min_kt = _SPLIT_MIN_KTILES
+    # fill the chip (a split only adds slab traffic); each split keeps >= 512 rows of K, 256
+    # under bf16, whose workgroups finish a k-tile several times faster (bf16 Depthformer
+    # 78.95 -> 77.44 ms; fp32 NeW-CRFs unchanged, AdaBins within noise; 128 slower again --
+    # tools/gpu_r4r.sh, gpu_r4s.sh, profiles/round4/ab_split_min_rows.txt)
+    min_kt = _SPLIT_MIN_KTILES if get_matmul_precision() == "bf16" else 32
     if tiles >= 384 or ktiles < min_kt:
         return 1
     target, cap = (_target_blocks(), 128) if tiles >= 8 else (2 * _target_blocks(), 512)
@@ -54,7 +58,7 @@ def _split_for(M, N, K):
     return max(1, split)
 
 
-_SPLIT_MIN_KTILES = int(os.environ.get("MDEMI_SPLIT_MIN_KTILES", "16"))  # K tiles of 16 rows
+_SPLIT_MIN_KTILES = int(os.environ.get("MDEMI_SPLIT_MIN_KTILES", "16"))  # bf16; K tiles of 16 rows
 
 
 def _draw_seed(device):
