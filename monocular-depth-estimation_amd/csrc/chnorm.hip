@@ -203,7 +203,8 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 
 // PASS 0: sum x; PASS 1: sum (x - mean)^2; PASS 2 (backward): (sum d*xhat, sum d) with
 // d = dy * act'(pre), pre = xhat * gamma + beta recomputed.  part: [blk][NV][C].
-template <int PASS>
+// ACT >= 0: the activation fixed at compile time (no per-element switch); -1: runtime `act`.
+template <int PASS, int ACT = -1>
 __global__ __launch_bounds__(CN_THREADS) void bn_partial4(const float* __restrict__ x, const float* __restrict__ dy,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ rstd,
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(CN_THREADS) void bn_partial4(const float* __restric
                                                           int64_t rows, int C, int act, int64_t rows_per_blk) {
   constexpr int NV = PASS == 2 ? 2 : 1;
   __shared__ float4 red[NV][CN_THREADS];
+  if (ACT >= 0) act = ACT;
   const int CQ = C >> 2, tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
   const int64_t r1 = min(rows, r0 + rows_per_blk);
@@ -323,10 +325,12 @@ __global__ __launch_bounds__(256) void bn_combine4(const float* __restrict__ par
   }
 }
 
+template <int ACT = -1>
 __global__ __launch_bounds__(CN_THREADS) void bn_apply4(const float* __restrict__ x, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, float* __restrict__ y,
                                                         int64_t total4, int CQ, int act) {
+  if (ACT >= 0) act = ACT;
   for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
     const int c = 4 * (int)(e % CQ);
     const float4 v = reinterpret_cast<const float4*>(x)[e];
@@ -340,6 +344,7 @@ __global__ __launch_bounds__(CN_THREADS) void bn_apply4(const float* __restrict_
   }
 }
 
+template <int ACT = -1>
 __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply4(const float* __restrict__ dy, const float* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
@@ -348,6 +353,7 @@ __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply4(const float* __restr
                                                             const float* __restrict__ dgamma,
                                                             const float* __restrict__ dbeta, float* __restrict__ dx,
                                                             int64_t total4, int CQ, float inv_n, int act) {
+  if (ACT >= 0) act = ACT;
   for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
     const int c = 4 * (int)(e % CQ);
     const float4 v = reinterpret_cast<const float4*>(x)[e];
@@ -388,6 +394,20 @@ static int grid_for(int64_t total) {
 
 using namespace mdemi;
 
+// launch KERNEL specialised on the activations the models use (BatchNormAct2d SiLU,
+// DecoderBN LeakyReLU, ConvModule ReLU, none); any other code takes the runtime switch
+#define MDEMI_BN_ACT_LAUNCH(KT, act, grid, ...)                                                   \
+  switch (act) {                                                                                \
+    case MDEMI_ACT_NONE: hipLaunchKernelGGL((KT(MDEMI_ACT_NONE)), grid, __VA_ARGS__); break;    \
+    case MDEMI_ACT_RELU: hipLaunchKernelGGL((KT(MDEMI_ACT_RELU)), grid, __VA_ARGS__); break;    \
+    case MDEMI_ACT_LEAKY: hipLaunchKernelGGL((KT(MDEMI_ACT_LEAKY)), grid, __VA_ARGS__); break;  \
+    case MDEMI_ACT_SILU: hipLaunchKernelGGL((KT(MDEMI_ACT_SILU)), grid, __VA_ARGS__); break;    \
+    default: hipLaunchKernelGGL((KT(-1)), grid, __VA_ARGS__); break;                            \
+  }
+#define MDEMI_KT_APPLY4(A) bn_apply4<A>
+#define MDEMI_KT_BWDAPPLY4(A) bn_bwd_apply4<A>
+#define MDEMI_KT_PARTIAL4_2(A) bn_partial4<2, A>
+
 extern "C" size_t mdemi_chnorm_workspace_size(int32_t N, int64_t HW, int32_t C, int32_t groups, int32_t is_bn) {
   (void)groups;
   if (is_bn) {
@@ -422,8 +442,8 @@ extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float*
                          rows, C, act, rpb4);
       hipLaunchKernelGGL(bn_combine4<1>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, rstd, nullptr);
       const int64_t total4 = rows * C / 4;
-      hipLaunchKernelGGL(bn_apply4, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, x, gamma, beta, mean, rstd, y,
-                         total4, C / 4, act);
+      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_APPLY4, act, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, x, gamma, beta, mean,
+                          rstd, y, total4, C / 4, act);
       return check_launch("chnorm_fwd");
     }
     const int rpb = rows_per_block(rows);
@@ -470,13 +490,13 @@ extern "C" int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y,
     if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
       const int nb = bn4_blocks(rows);
       const int64_t rpb4 = cdiv(rows, nb);
-      hipLaunchKernelGGL(bn_partial4<2>, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta, part, rows,
-                         C, act, rpb4);
+      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_PARTIAL4_2, act, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta,
+                          part, rows, C, act, rpb4);
       hipLaunchKernelGGL(bn_combine4<2>, dim3(bn4_combine_grid(C)), dim3(256), 0, st, part, nb, C, rows, 0.f, dgamma,
                          dbeta);
       const int64_t total4 = rows * C / 4;
-      hipLaunchKernelGGL(bn_bwd_apply4, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma, beta,
-                         dgamma, dbeta, dx, total4, C / 4, 1.f / (float)rows, act);
+      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_BWDAPPLY4, act, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd,
+                          gamma, beta, dgamma, dbeta, dx, total4, C / 4, 1.f / (float)rows, act);
       return check_launch("chnorm_bwd");
     }
     const int rpb = rows_per_block(rows);
@@ -563,8 +583,8 @@ extern "C" int mdemi_bn_frozen_bwd(const float* dy, const float* x, const float*
     float* part = (float*)workspace;
     if (vec) {
       const int nb = bn4_blocks(rows);
-      hipLaunchKernelGGL(bn_partial4<2>, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta, part, rows,
-                         C, act, cdiv(rows, nb));
+      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_PARTIAL4_2, act, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta,
+                          part, rows, C, act, cdiv(rows, nb));
       hipLaunchKernelGGL(bn_combine4<2>, dim3(bn4_combine_grid(C)), dim3(256), 0, st, part, nb, C, rows, 0.f, dgamma,
                          dbeta);
     } else {
