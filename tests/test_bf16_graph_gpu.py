@@ -30,8 +30,9 @@ BF16_OUT_L2, BF16_GRAD_L2 = 1e-2, 1e-1
 BF16_EMU_GRAD_L2 = 1e-2
 # a gradient whose bf16 rounding noise (bf16-emulating fp64 oracle vs the un-rounded fp64
 # oracle) is at least this fraction of its size is decided by where roundings fall, not by
-# the arithmetic: held to lie within BF16_NOISE_BALL x that noise of the emulation
-BF16_NOISE_DOMINATED, BF16_NOISE_BALL = 0.1, 2.0
+# the arithmetic: the GPU's distance from the exact (un-rounded) gradient is held to
+# BF16_NOISE_BALL x the emulation's own distance from it
+BF16_NOISE_DOMINATED, BF16_NOISE_BALL = 0.1, 3.0
 
 
 @pytest.fixture(scope="module")
@@ -240,9 +241,12 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf, bn):
     emulation itself moves the gradient by more than its size (measured on the CPU, train-mode
     BN: luna_layers.2.luna_attn.v1_proj.bias relative L2 3.49 between the bf16-emulating and the
     un-rounded fp64 oracle).  So the noise n = ||o64 - plain64|| / ||o64|| is measured per
-    parameter, and a gradient with n >= BF16_NOISE_DOMINATED is held to
-        ||gpu - o64|| / ||o64|| <= BF16_NOISE_BALL x n
-    (the GPU's rounding lands inside the emulation's noise ball), while every other gradient
+    parameter, and a gradient with n >= BF16_NOISE_DOMINATED is held against the exact value:
+        ||gpu - plain64|| <= BF16_NOISE_BALL x ||o64 - plain64||
+    (the GPU's rounding moves it no farther from the exact gradient than 3x what the same
+    rounding does in the emulation; GPU and emulation round different fp32 values, so their
+    residues are independent draws and can differ from each other by more than either's
+    size -- measured 1.3-1.9 x n between builds that only reorder fp32 sums), while every other gradient
     -- a wrong or missing term on a well-conditioned gradient -- takes the bound above.
 
     What bf16 itself costs against the fp32 model is reported beside it: depth and centres
@@ -309,15 +313,20 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf, bn):
         l2 = lambda a: torch.linalg.norm(a).item()  # noqa: E731
         ref = l2(r64) + 1e-300
         diag.append((l2(g - r64) / ref, l2(r32.double() - r64) / ref, l2(Pplain[k].grad - r64) / ref,
-                     l2(r64) / r64.numel() ** 0.5, k))
+                     l2(r64) / r64.numel() ** 0.5, k, l2(g - Pplain[k].grad) / ref))
     assert n == len(list(m.parameters()))
     for d in sorted(diag, reverse=True)[:12]:
         print(f"  grad rel-L2 gpu {d[0]:.3e}  cpu32 {d[1]:.3e}  bf16 noise {d[2]:.3e}  rms {d[3]:.3e}  {d[4]}")
-    bad = [(k, e_gpu, e_cpu, noise) for e_gpu, e_cpu, noise, _, k in diag
+    tight = [d for d in diag if d[0] <= 20.0 * d[1] + BF16_EMU_GRAD_L2]
+    bad = [(k, e_gpu, e_cpu, noise, g_plain) for e_gpu, e_cpu, noise, _, k, g_plain in diag
            if e_gpu > 20.0 * e_cpu + BF16_EMU_GRAD_L2 and
-           not (noise >= BF16_NOISE_DOMINATED and e_gpu <= BF16_NOISE_BALL * noise)]
-    noisy = sum(1 for d in diag if d[2] >= BF16_NOISE_DOMINATED)
-    print(f"  {noisy} of {len(diag)} gradients bf16-noise-dominated; beyond the bounds: {bad}")
+           not (noise >= BF16_NOISE_DOMINATED and g_plain <= BF16_NOISE_BALL * noise)]
+    noisy = [d for d in diag if d[2] >= BF16_NOISE_DOMINATED]
+    ball = [d for d in diag if d not in tight]
+    for d in sorted(ball, key=lambda d: -d[5] / max(d[2], 1e-300))[:8]:
+        print(f"  noise-ball: |gpu-exact| {d[5]:.3e}  |emu-exact| {d[2]:.3e}  ratio {d[5] / max(d[2], 1e-300):.2f}  {d[4]}")
+    print(f"  {len(noisy)} of {len(diag)} gradients bf16-noise-dominated; {len(tight)} within the tight bound, "
+          f"{len(ball) - len(bad)} by the noise ball; beyond the bounds: {bad}")
     assert not bad, bad
 
     def rel_l2(a, r):
