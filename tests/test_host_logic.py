@@ -40,3 +40,21 @@ def test_running_average_dict():
     d.reset()
     d.update({"a1": 0.25, "rmse": 1.0})
     assert d.get_value() == {"a1": 0.25, "rmse": 1.0}
+
+
+def test_split_k_plan():
+    """Split-K planning (mdemi.functional._split_for): no split once >= 384 output tiles fill the
+    chip or the reduction is short; skinny outputs split deep; bf16 keeps >= 256 K rows per
+    split where fp32 keeps >= 512 (profiles/round4/ab_split_min_rows.txt)."""
+    from mdemi import functional as mf
+    assert mf._split_for(9600, 3072, 768) == 1          # 75 x 24 tiles
+    assert mf._split_for(128, 128, 400) == 1            # 25 K tiles: too short to split
+    fp32 = mf._split_for(768, 128, 9600)                # 6 tiles, 600 K tiles
+    assert fp32 == 600 // 32
+    with mf.matmul_precision("bf16"):
+        bf16 = mf._split_for(768, 128, 9600)
+    assert bf16 == 600 // 16 and bf16 > fp32
+    assert mf._split_for(24, 40, 300000) == 512         # skinny: capped at 512 slabs
+    for M, N, K in ((768, 768, 9600), (64, 792, 614400), (2304, 768, 9600)):
+        s = mf._split_for(M, N, K)
+        assert 1 <= s <= 512 and K / s >= 512 - 16
