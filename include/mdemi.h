@@ -335,6 +335,14 @@ int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y, const floa
 int mdemi_chnorm_apply(const float* x, const float* gamma, const float* beta, const float* mean,
                        const float* rstd, float* y, int32_t N, int64_t HW, int32_t C, int32_t groups,
                        int32_t is_bn, int32_t act, void* stream);
+/* training-mode BatchNorm2d forward (mdemi_chnorm_fwd with is_bn = 1) that also applies the
+ * running-statistics update of mdemi_bn_running_update (momentum, num_batches_tracked += 1
+ * when given) inside its statistics pass: nn.BatchNorm2d.forward in train mode in one call
+ * (uper_crf_head.py:341-348 ConvModule, unet_adaptive_bins.py:13,16, layer_utils.py:25). */
+int mdemi_bn_train_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean,
+                       float* rstd, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                       float momentum, int32_t N, int64_t HW, int32_t C, float eps, int32_t act,
+                       void* workspace, void* stream);
 /* backward of mdemi_chnorm_apply for BatchNorm (eval-mode BN inside a training step:
  * frozen statistics, so dx = gamma * rstd * act'(pre) * dy with no batch terms);
  * dx may be NULL (input needs no gradient); dgamma and dbeta are both NULL (frozen

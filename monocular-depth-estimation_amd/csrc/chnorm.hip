@@ -283,9 +283,24 @@ __global__ __launch_bounds__(CN_THREADS) void bn_partial4(const float* __restric
 // partial rows), then folds lanes and accumulators in a fixed order.
 // MODE 0: mean = s / rows; MODE 1: rstd = 1 / sqrt(s / rows + eps);
 // MODE 2: (dgamma, dbeta) from [blk][2][C].
+// nn.BatchNorm2d's running-statistics update (unbiased batch variance, momentum m), done by
+// the rstd combine when rmean is set: one launch fewer per training-mode BN
+struct BnRunning {
+  float* rmean;
+  float* rvar;
+  int64_t* tracked;  // num_batches_tracked (+1), may be null
+  float unbias, m;
+};
+__device__ __forceinline__ void bn_running_one(const BnRunning& run, float mu, float r, float eps, int c) {
+  const float var = (1.f / (r * r) - eps) * run.unbias;
+  run.rmean[c] = (1.f - run.m) * run.rmean[c] + run.m * mu;
+  run.rvar[c] = (1.f - run.m) * run.rvar[c] + run.m * var;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_combine4(const float* __restrict__ part, int nblk, int C, int64_t rows,
-                                                   float eps, float* __restrict__ out0, float* __restrict__ out1) {
+                                                   float eps, float* __restrict__ out0, float* __restrict__ out1,
+                                                   BnRunning run = BnRunning{}, const float* __restrict__ mean = nullptr) {
   constexpr int NV = MODE == 2 ? 2 : 1;
   __shared__ double red[NV][256];
   const int cpb = C < 16 ? C : 16, lpc = 256 / cpb;
@@ -307,6 +322,7 @@ __global__ __launch_bounds__(256) void bn_combine4(const float* __restrict__ par
       if (NV == 2) b[0] += (double)part[(int64_t)i * stride + C + c];
     }
   }
+  if (MODE == 1 && run.tracked && blockIdx.x == 0 && threadIdx.x == 0) run.tracked[0] += 1;
   red[0][threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
   if (NV == 2) red[NV - 1][threadIdx.x] = (b[0] + b[1]) + (b[2] + b[3]);
   __syncthreads();
@@ -317,8 +333,11 @@ __global__ __launch_bounds__(256) void bn_combine4(const float* __restrict__ par
       if (NV == 2) sb += red[NV - 1][k * cpb + cl];
     }
     if (MODE == 0) out0[c] = (float)(sa / (double)rows);
-    else if (MODE == 1) out0[c] = (float)(1.0 / sqrt(sa / (double)rows + (double)eps));
-    else {
+    else if (MODE == 1) {
+      const float r = (float)(1.0 / sqrt(sa / (double)rows + (double)eps));
+      out0[c] = r;
+      if (run.rmean) bn_running_one(run, mean[c], r, eps, c);
+    } else {
       out0[c] = (float)sa;
       out1[c] = (float)sb;
     }
@@ -419,9 +438,20 @@ extern "C" size_t mdemi_chnorm_workspace_size(int32_t N, int64_t HW, int32_t C, 
   return (size_t)N * 2 * C * sizeof(float);
 }
 
-extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean,
-                                float* rstd, int32_t N, int64_t HW, int32_t C, int32_t groups, int32_t is_bn, float eps,
-                                int32_t act, void* workspace, void* stream) {
+__global__ void bn_running_kernel(const float* __restrict__ mean, const float* __restrict__ rstd,
+                                  float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ tracked,
+                                  int C, float unbias, float eps, float m) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tracked && c == 0) tracked[0] += 1;  // nn.BatchNorm2d.num_batches_tracked
+  if (c >= C) return;
+  bn_running_one(BnRunning{rmean, rvar, nullptr, unbias, m}, mean[c], rstd[c], eps, c);
+}
+
+static float bn_unbias(int64_t rows) { return (float)((double)rows / (double)(rows > 1 ? rows - 1 : 1)); }
+
+static int chnorm_fwd_impl(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
+                           int32_t N, int64_t HW, int32_t C, int32_t groups, int32_t is_bn, float eps, int32_t act,
+                           void* workspace, void* stream, BnRunning run) {
   MDEMI_REQUIRE(x && gamma && beta && y && mean && rstd && N > 0 && HW > 0 && C > 0, "chnorm_fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   if (is_bn) {
@@ -440,7 +470,8 @@ extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float*
       hipLaunchKernelGGL(bn_combine4<0>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, mean, nullptr);
       hipLaunchKernelGGL(bn_partial4<1>, dim3(nb), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma, beta, part,
                          rows, C, act, rpb4);
-      hipLaunchKernelGGL(bn_combine4<1>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, rstd, nullptr);
+      hipLaunchKernelGGL(bn_combine4<1>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, rstd, nullptr, run,
+                         (const float*)mean);
       const int64_t total4 = rows * C / 4;
       MDEMI_BN_ACT_LAUNCH(MDEMI_KT_APPLY4, act, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, x, gamma, beta, mean,
                           rstd, y, total4, C / 4, act);
@@ -454,6 +485,9 @@ extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float*
     hipLaunchKernelGGL(bn_combine, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, rows, 1, eps, mean, rstd);
     hipLaunchKernelGGL(chnorm_apply, dim3(grid_for(rows * C)), dim3(CN_THREADS), 0, st, x, gamma, beta, mean, rstd, y,
                        N, HW, C, C, 1, act);
+    if (run.rmean)
+      hipLaunchKernelGGL(bn_running_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, mean, rstd, run.rmean,
+                         run.rvar, run.tracked, C, run.unbias, eps, run.m);
   } else {
     MDEMI_REQUIRE(groups > 0 && C % groups == 0, "chnorm_fwd: C %% groups != 0");
     hipLaunchKernelGGL(gn_stats, dim3(N * groups), dim3(CN_THREADS), 0, st, x, mean, rstd, HW, C, groups, eps);
@@ -461,6 +495,23 @@ extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float*
                        mean, rstd, y, N, HW, C, groups, 0, act);
   }
   return check_launch("chnorm_fwd");
+}
+
+extern "C" int mdemi_chnorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean,
+                                float* rstd, int32_t N, int64_t HW, int32_t C, int32_t groups, int32_t is_bn, float eps,
+                                int32_t act, void* workspace, void* stream) {
+  return chnorm_fwd_impl(x, gamma, beta, y, mean, rstd, N, HW, C, groups, is_bn, eps, act, workspace, stream,
+                         BnRunning{});
+}
+
+extern "C" int mdemi_bn_train_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean,
+                                  float* rstd, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                                  float momentum, int32_t N, int64_t HW, int32_t C, float eps, int32_t act,
+                                  void* workspace, void* stream) {
+  MDEMI_REQUIRE(running_mean && running_var, "bn_train_fwd: running statistics required");
+  const int64_t rows = (int64_t)N * HW;
+  return chnorm_fwd_impl(x, gamma, beta, y, mean, rstd, N, HW, C, C, 1, eps, act, workspace, stream,
+                         BnRunning{running_mean, running_var, num_batches_tracked, bn_unbias(rows), momentum});
 }
 
 __global__ void gn_param_reduce(const float* __restrict__ part, int N, int C, float* dgamma, float* dbeta) {
@@ -608,23 +659,11 @@ extern "C" int mdemi_bn_frozen_bwd(const float* dy, const float* x, const float*
   return check_launch("bn_frozen_bwd");
 }
 
-__global__ void bn_running_kernel(const float* __restrict__ mean, const float* __restrict__ rstd,
-                                  float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ tracked,
-                                  int C, float unbias, float eps, float m) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tracked && c == 0) tracked[0] += 1;  // nn.BatchNorm2d.num_batches_tracked
-  if (c >= C) return;
-  const float r = rstd[c];
-  const float var = (1.f / (r * r) - eps) * unbias;
-  rmean[c] = (1.f - m) * rmean[c] + m * mean[c];
-  rvar[c] = (1.f - m) * rvar[c] + m * var;
-}
-
 extern "C" int mdemi_bn_running_update(const float* mean, const float* rstd, float* running_mean, float* running_var,
                                        int64_t* num_batches_tracked, int32_t C, int64_t rows, float eps,
                                        float momentum, void* stream) {
   MDEMI_REQUIRE(mean && rstd && running_mean && running_var && C > 0 && rows > 0, "bn_running_update: bad args");
-  const float unbias = (float)((double)rows / (double)(rows > 1 ? rows - 1 : 1));
+  const float unbias = bn_unbias(rows);
   hipLaunchKernelGGL(bn_running_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, mean, rstd,
                      running_mean, running_var, num_batches_tracked, C, unbias, eps, momentum);
   return check_launch("bn_running_update");

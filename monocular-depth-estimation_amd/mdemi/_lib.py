@@ -156,6 +156,7 @@ _SIGS = {
     "mdemi_copy2d": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, i32, vp]),
     "mdemi_chnorm_apply": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp]),
     "mdemi_bn_frozen_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, vp, vp]),
+    "mdemi_bn_train_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i64, i32, f32, i32, vp, vp]),
     "mdemi_bn_running_update": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i64, f32, f32, vp]),
     "mdemi_multi_tensor_chunk": (ctypes.c_int, []),
     "mdemi_grad_norm_workspace_size": (sz, [i32]),

@@ -948,7 +948,9 @@ def nhwc_to_nchw(x):
 
 class _ChNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, groups, is_bn, eps, act):
+    def forward(ctx, x, weight, bias, groups, is_bn, eps, act, running=None):
+        """running: (running_mean, running_var, num_batches_tracked or None, momentum) -- the
+        BatchNorm running-statistics update done by the same call (mdemi_bn_train_fwd)."""
         _require_cuda(x, weight, bias)
         x = _c(x)
         n = x.shape[0]
@@ -960,9 +962,16 @@ class _ChNormFn(torch.autograd.Function):
         rstd = torch.empty(nstat, device=x.device, dtype=torch.float32)
         lib = L.load()
         ws = L.workspace(lib.mdemi_chnorm_workspace_size(n, hw, c, groups, int(is_bn)), x.device)
-        L.check(lib.mdemi_chnorm_fwd(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(), mean.data_ptr(),
-                                     rstd.data_ptr(), n, hw, c, groups, int(is_bn), float(eps), act, ws.data_ptr(),
-                                     L.stream()), "chnorm_fwd")
+        if running is not None:
+            rm, rv, tracked, momentum = running
+            L.check(lib.mdemi_bn_train_fwd(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
+                                           mean.data_ptr(), rstd.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+                                           L.ptr(tracked), float(momentum), n, hw, c, float(eps), act,
+                                           ws.data_ptr(), L.stream()), "bn_train_fwd")
+        else:
+            L.check(lib.mdemi_chnorm_fwd(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
+                                         mean.data_ptr(), rstd.data_ptr(), n, hw, c, groups, int(is_bn), float(eps),
+                                         act, ws.data_ptr(), L.stream()), "chnorm_fwd")
         ctx.save_for_backward(x, weight, bias, mean, rstd)
         ctx.cfg = (groups, is_bn, act)
         ctx.mark_non_differentiable(mean, rstd)
@@ -972,7 +981,7 @@ class _ChNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dm, _dr):
         if dy is None:
-            return None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         x, weight, bias, mean, rstd = ctx.saved_tensors
         groups, is_bn, act = ctx.cfg
         dy = _c(dy)
@@ -987,12 +996,14 @@ class _ChNormFn(torch.autograd.Function):
         L.check(lib.mdemi_chnorm_bwd(dy.data_ptr(), x.data_ptr(), None, mean.data_ptr(), rstd.data_ptr(),
                                      weight.data_ptr(), bias.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(),
                                      n, hw, c, groups, int(is_bn), act, ws.data_ptr(), L.stream()), "chnorm_bwd")
-        return dx, dg, db, None, None, None, None
+        return dx, dg, db, None, None, None, None, None
 
 
-def batch_norm_nhwc(x, weight, bias, eps=1e-5, act=L.ACT_NONE):
-    """Training-mode BatchNorm2d over an NHWC map; returns (y, batch_mean, batch_rstd)."""
-    return _ChNormFn.apply(x, weight, bias, x.shape[-1], True, eps, act)
+def batch_norm_nhwc(x, weight, bias, eps=1e-5, act=L.ACT_NONE, running=None):
+    """Training-mode BatchNorm2d over an NHWC map; returns (y, batch_mean, batch_rstd).
+    running=(running_mean, running_var, num_batches_tracked or None, momentum) also applies
+    nn.BatchNorm2d's running-statistics update in the same call."""
+    return _ChNormFn.apply(x, weight, bias, x.shape[-1], True, eps, act, running)
 
 
 def group_norm_nhwc(x, weight, bias, groups, eps=1e-5, act=L.ACT_NONE):

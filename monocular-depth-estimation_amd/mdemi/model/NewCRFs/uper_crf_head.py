@@ -51,17 +51,19 @@ def bn_forward(bn: nn.BatchNorm2d, x, act=L.ACT_NONE):
     """nn.BatchNorm2d semantics on an NHWC map: batch statistics + running-stat
     update in training, running statistics in eval."""
     if bn.training or not bn.track_running_stats:
+        if bn.track_running_stats and bn.momentum is not None:  # statistics + running update, one call
+            y, _, _ = mf.batch_norm_nhwc(x, bn.weight, bn.bias, bn.eps, act,
+                                         running=(bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                                                  bn.momentum))
+            return y
         y, mean, rstd = mf.batch_norm_nhwc(x, bn.weight, bn.bias, bn.eps, act)
-        if bn.track_running_stats:
+        if bn.track_running_stats:  # cumulative average (momentum None): needs the count on the host
             with torch.no_grad():
                 n = x.numel() // x.shape[-1]
-                if bn.momentum is None:  # cumulative average: needs the count on the host
-                    bn.num_batches_tracked.add_(1)
-                    m, tracked = 1.0 / float(bn.num_batches_tracked), None
-                else:  # the counter rides on the update launch
-                    m, tracked = bn.momentum, bn.num_batches_tracked.data_ptr()
+                bn.num_batches_tracked.add_(1)
+                m = 1.0 / float(bn.num_batches_tracked)
                 L.call("mdemi_bn_running_update", mean.data_ptr(), rstd.data_ptr(), bn.running_mean.data_ptr(),
-                       bn.running_var.data_ptr(), tracked, x.shape[-1], n, float(bn.eps), float(m), L.stream())
+                       bn.running_var.data_ptr(), None, x.shape[-1], n, float(bn.eps), float(m), L.stream())
         return y
     return mf.batch_norm_eval_nhwc(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, act)
 
