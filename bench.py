@@ -143,6 +143,14 @@ def parse():
                          "fp32 via three exact bf16 planes on the bf16 MFMA (fp32 error); bf16: bf16 operands, "
                          "fp32 accumulate")
     ap.add_argument("--graph", action="store_true", help="capture the whole train step in a hipGraph")
+    ap.add_argument("--data", default="synthetic", choices=["synthetic", "synthetic-files"],
+                    help="synthetic-files: also time the real-data front end -- NYU-format JPEG/PNG files "
+                         "decoded by DepthDataset in DataLoader workers, collate_raw, GpuSampleTransform on "
+                         "the GPU -- feeding the same train step (reported beside the synthetic rate)")
+    ap.add_argument("--data-workers", type=int, default=4)
+    ap.add_argument("--ddp", action="store_true",
+                    help="N = 1: run the data-parallel step anyway -- a world-1 RCCL group, GradAllReduce "
+                         "buckets and their all-reduces (the N > 1 code path on one GPU)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: launcher/gloo plumbing check only (a toy model, not a measurement)")
     return ap.parse_args()
@@ -194,6 +202,97 @@ def synthetic_batch(B, H, W, device, seed, data_type="NYU"):
         gt = torch.rand(B, 1, H, W, generator=g) * 79.0 + 1.0
         valid = (torch.rand(B, 1, H, W, generator=g) < 0.15).float()
     return img.to(device), (gt * valid).to(device)
+
+
+# --------------------------------------------------------------------------- real-data front end
+class FilePipeline:
+    """SURVEY §8f-2 / dataset/depth_dataset.py:166-284 on files: `n_files` synthetic NYU-format
+    frames written once to a temporary directory (RGB JPEG, quality 95, and a 16-bit PNG depth
+    in millimetres, saving_factor 1000 -- the reference's NYU layout), then per step
+    DepthDataset.__getitem__ (Pillow decode) in `workers` DataLoader worker processes,
+    collate_raw into pinned host batches, and GpuSampleTransform (rotate, crop, flip, colour
+    augmentation, normalisation: one libmdemi sweep) on the GPU.  The workers are forked here,
+    before this process touches the GPU, and only decode."""
+
+    def __init__(self, B, H, W, data_type, n_files, workers, seed=0):
+        import tempfile
+
+        import numpy as np
+        from PIL import Image
+        from mdemi.dataset import DepthDataset, collate_raw
+        if data_type != "NYU":
+            raise SystemExit("bench: --data synthetic-files writes NYU-format frames (the default workload)")
+        self.tmp = tempfile.TemporaryDirectory(prefix="mdemi_bench_files_")
+        rng = np.random.default_rng(seed)
+        yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+        names = []
+        for i in range(n_files):  # smooth colour fields + noise (JPEG sizes like photographs') and a depth ramp
+            ph = rng.uniform(0, 6.28, 3)
+            rgb = np.stack([127 + 80 * np.sin(xx / (37 + 11 * c) + yy / (53 - 7 * c) + ph[c]) for c in range(3)], -1)
+            rgb = np.clip(rgb + rng.normal(0, 12, rgb.shape), 0, 255).astype(np.uint8)
+            dep = (1000 * (0.5 + 9.0 * (xx / W) * (0.6 + 0.4 * np.sin(yy / 41 + ph[0])) ** 2)).astype(np.uint16)
+            Image.fromarray(rgb).save(os.path.join(self.tmp.name, f"rgb_{i:04d}.jpg"), quality=95)
+            Image.fromarray(dep).save(os.path.join(self.tmp.name, f"sync_depth_{i:04d}.png"))
+            names.append(f"/rgb_{i:04d}.jpg /sync_depth_{i:04d}.png 518.8579\n")
+        self.bytes_on_disk = sum(os.path.getsize(os.path.join(self.tmp.name, f)) for f in os.listdir(self.tmp.name))
+        self.ds = DepthDataset(self.tmp.name, "NYU", "train", img_size=(H, W), filenames=names)
+        sampler = torch.utils.data.RandomSampler(self.ds, replacement=True, num_samples=1 << 30,
+                                                 generator=torch.Generator().manual_seed(seed))
+        self.loader = torch.utils.data.DataLoader(self.ds, batch_size=B, sampler=sampler, num_workers=workers,
+                                                  collate_fn=collate_raw, pin_memory=True, drop_last=True,
+                                                  persistent_workers=workers > 0, prefetch_factor=4 if workers else None,
+                                                  multiprocessing_context="fork" if workers else None)
+        self.it = iter(self.loader)  # forks the workers now (before any HIP call in this process)
+        self.n_files, self.workers = n_files, workers
+        self.tf = None
+
+    def next(self):
+        import random as _random
+        if self.tf is None:
+            self.tf = self.ds.transform()
+            self.rnd = _random.Random(0)
+        b = next(self.it)
+        img, gt, _ = self.tf(b["image"], b["depth"], rnd=self.rnd)
+        return img, gt
+
+    def close(self):
+        del self.it
+        self.tmp.cleanup()
+
+
+def measure_files(args, trainer, pipe, B, world):
+    """The train step fed from the file pipeline: W warm-up steps, then K timed steps
+    (barrier + synchronize on both sides, as in measure), each = next decoded batch ->
+    GpuSampleTransform -> Trainer.step.  Also the front end alone over K batches."""
+    na = trainer.num_accum
+    for _ in range(max(args.warmup, 1)):
+        trainer.step([pipe.next() for _ in range(na)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step([pipe.next() for _ in range(na)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    t0 = time.perf_counter()  # front end alone: decode (workers) + pinned H2D + augment sweep
+    for _ in range(args.steps):
+        pipe.next()
+    torch.cuda.synchronize()
+    fe = time.perf_counter() - t0
+    return {"images_per_sec": round(B * na * world * args.steps / elapsed, 3),
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "front_end_alone_images_per_sec": round(B * na * args.steps / fe, 2),
+            "workers": pipe.workers, "files": pipe.n_files, "bytes_on_disk": pipe.bytes_on_disk,
+            "pipeline": "DepthDataset.__getitem__ (Pillow JPEG/PNG decode, DataLoader workers) -> collate_raw "
+                        "(pinned) -> GpuSampleTransform (mdemi_augment: rotate/crop/flip/colour/normalise) -> "
+                        "Trainer.step"}
 
 
 # --------------------------------------------------------------------------- roofline
@@ -483,7 +582,8 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
     opt = copy.deepcopy(opt)
     opt["dataloader"]["batch_size"] = B
     torch.manual_seed(0)
-    trainer = build_from_config(opt, device=device, world=world, precision=precision, graph=graph)
+    trainer = build_from_config(opt, device=device, world=world, precision=precision, graph=graph,
+                                ddp=(True if getattr(args, "ddp", False) else None))
     na = trainer.num_accum
     batches = [synthetic_batch(B, H, W, device, seed=1000 + 7 * rank + i, data_type=opt["dataset"]["data_type"])
                for i in range(na)]
@@ -509,7 +609,7 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
         elapsed = t.item()
     res = {"elapsed": elapsed, "ms": elapsed / args.steps * 1e3, "images": B * na * world * args.steps,
            "loss": float(loss.item()), "num_accum": na, "trainer": trainer}
-    if world > 1:  # isolated cost of the whole gradient exchange (no overlap): an upper bound on exposed comm
+    if trainer.ddp is not None:  # isolated cost of the whole gradient exchange (no overlap): an upper bound on exposed comm
         ddp = trainer.ddp
         torch.cuda.synchronize()
         dist.barrier()
@@ -520,7 +620,8 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
         iso = (time.perf_counter() - t0) / 3 * 1e3
         res["allreduce"] = {"grad_bytes": sum(ddp.bucket_bytes), "buckets": len(ddp.buckets),
                             "isolated_ms": round(iso, 2), "share_of_step_upper_bound": round(iso / res["ms"], 4),
-                            "bus_GBps": round(2 * (world - 1) / world * sum(ddp.bucket_bytes) / (iso * 1e-3) / 1e9, 1)}
+                            "bus_GBps": round(2 * (world - 1) / world * sum(ddp.bucket_bytes) / (iso * 1e-3) / 1e9, 1),
+                            "last_launch_order": ddp.last_launch_order}
     _progress(f"{key}: {res['ms']:.1f} ms/step")
     if with_roofline:
         res["roofline"], res["extra"] = roofline_entry(trainer, batches, key, res["ms"])
@@ -633,12 +734,23 @@ def main():
         sys.exit(2)
     if args.device == "cpu":
         return plumbing_main(args, rank, world)
+    pipe = None
+    if args.data == "synthetic-files":  # before any GPU call: the decode workers fork here
+        wl0 = WORKLOADS[args.model] if not args.config else None
+        if wl0 is None:
+            raise SystemExit("bench: --data synthetic-files runs the --model workloads")
+        B0 = args.batch or int(wl0["opt"]["dataloader"]["batch_size"])
+        pipe = FilePipeline(B0, args.height or wl0["h"], args.width or wl0["w"], wl0["opt"]["dataset"]["data_type"],
+                            n_files=max(4 * B0, 32), workers=args.data_workers, seed=rank)
+        _progress(f"file pipeline: {pipe.n_files} frames written, {pipe.workers} decode workers")
     if local >= torch.cuda.device_count():
         print(f"bench: local rank {local} has no GPU ({torch.cuda.device_count()} visible)", file=sys.stderr)
         sys.exit(2)
-    if world > 1:
+    if world > 1 or args.ddp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
+        if world == 1 and "MASTER_PORT" not in os.environ:  # --ddp without a launcher: a world-1 group
+            os.environ.update(MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         assert dist.get_world_size() == args.gpus
     device = torch.device("cuda", local)
@@ -664,6 +776,13 @@ def main():
     res = measure(args, opt, key, H, W, B, rank, world, device, with_roofline=not args.no_roofline,
                   precision=precision, graph=graph)
     value = res["images"] / res["elapsed"]
+    files = None
+    if pipe is not None:
+        _progress("file pipeline: timing")
+        files = measure_files(args, res["trainer"], pipe, B, world)
+        files["vs_synthetic"] = round(files["images_per_sec"] / value, 4)
+        pipe.close()
+        _progress(f"file pipeline: {files['images_per_sec']} img/s ({files['vs_synthetic']} of synthetic)")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(res["trainer"].model, opt, H, W, args.cpu_budget_s)
@@ -692,17 +811,19 @@ def main():
                        "parallelism": f"dp{world}", "reference_config": ref_cfg,
                        "matmul_precision": precision, "hipgraph": graph},
             "roofline": res.get("roofline"), "cpu_baseline": cpu, "loss": round(res["loss"], 5),
-            "rccl_world": world if world > 1 else None,
+            "rccl_world": world if (world > 1 or args.ddp) else None,
         }
         if "allreduce" in res:
             line["allreduce"] = res["allreduce"]
+        if files is not None:
+            line["data_pipeline"] = files
         line.update(res.get("extra", {}))
         if secondary:
             line["secondary"] = secondary.pop("newcrfs_kitti", None)
             if secondary:
                 line["secondaries"] = secondary
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -193,12 +193,23 @@ class OrderedSwinRegHead(nn.Module):
             for _ in range(num_repeats)])
         self.sigmoid = nn.Sigmoid()
 
+    # Validation path: the attention kernels clamp a depth index to [0, num_emb-1]
+    # (csrc/oda2.hip) where the reference's F.embedding would raise on the -1 a saturated
+    # logit (sigmoid == 0) produces.  With validate_indices set, every out-of-range index is
+    # counted on the device (clamped_indices, no host sync) so a test or a debugging run sees
+    # what the clamp hid; off by default (two extra sweeps of the index map per layer).
+    validate_indices = False
+
     @torch.no_grad()
     def _logit_to_indices(self, out):
         """:246-253 floor(sigmoid(logit) * n - 1e-3) (one elementwise sweep, then the cast)."""
         assert out.shape[-1] == 1
         s = mf.activation(out.detach(), L.ACT_SIGMOID)
-        return torch.floor(s * self.num_emb - 1e-3).to(torch.int32).squeeze(-1)
+        idx = torch.floor(s * self.num_emb - 1e-3).to(torch.int32).squeeze(-1)
+        if self.validate_indices:
+            bad = ((idx < 0) | (idx >= self.num_emb)).sum()
+            self.clamped_indices = bad if getattr(self, "clamped_indices", None) is None else self.clamped_indices + bad
+        return idx
 
     def forward_logits(self, x):
         """x: (B, H, W, C) -> (logits: num_repeats + 1 maps (B, H', W', 1), attn_weights)."""

@@ -170,27 +170,41 @@ def freeze_bn(model):
             m.eval()
 
 
-def quiesce_process_group(works=()):
-    """Before a hipGraph capture on a process whose RCCL process group has run eager
-    collectives: wait for each eager Work, then block until ProcessGroupNCCL's watchdog
-    thread has retired every one of them (ProcessGroupNCCL::waitForPendingWorks returns
-    once the watchdog's work list and its completed-work list are both empty).  The
-    watchdog polls each listed work's HIP event (hipEventQuery); such a query issued
+def quiesce_process_group(works=(), groups=()):
+    """Before a hipGraph capture on a process whose RCCL process groups have run eager
+    collectives: wait for each eager Work, then block until every ProcessGroupNCCL's
+    watchdog thread has retired every one of them (ProcessGroupNCCL::waitForPendingWorks
+    returns once the watchdog's work list and its completed-work list are both empty).
+    The watchdog polls each listed work's HIP event (hipEventQuery); such a query issued
     while this thread holds a global-mode capture is a capture-unsafe call from another
     thread, which invalidates the capture and aborts the process.  Collectives issued
-    during the capture are never listed, so once the list is empty nothing else can
-    query mid-capture.  A no-op without an initialised process group; gloo groups have
-    no watchdog (nothing to wait for)."""
+    during the capture are never listed, so once the lists are empty nothing else can
+    query mid-capture.  ``groups``: the process groups the captured step issues
+    collectives on besides the default one (GradAllReduce(group=...)); each "nccl" group
+    is drained.  A no-op without an initialised process group; gloo groups have no
+    watchdog (nothing to wait for).  The drain is a private ProcessGroupNCCL method
+    (torch 2.10: ``_wait_for_pending_works``); if a torch update removes it this raises
+    rather than capture without the guarantee."""
     import torch.distributed as dist
     for w in works:
         w.wait()
     torch.cuda.synchronize()
     if not (dist.is_available() and dist.is_initialized()):
         return
-    groups = [dist.distributed_c10d._get_default_group()]
-    for pg in groups:
-        if dist.get_backend(pg) == "nccl":
-            pg._wait_for_pending_works()
+    todo = [dist.distributed_c10d._get_default_group()]
+    for g in groups:
+        if g is not None and all(g is not t for t in todo):
+            todo.append(g)
+    for pg in todo:
+        if dist.get_backend(pg) != "nccl":
+            continue
+        drain = getattr(pg, "_wait_for_pending_works", None)
+        if drain is None:
+            raise RuntimeError(
+                f"quiesce_process_group: torch {torch.__version__}'s ProcessGroupNCCL has no "
+                "_wait_for_pending_works(); a global-mode hipGraph capture could race the RCCL "
+                "watchdog's event queries -- capture refused (run the step eagerly: graph=False)")
+        drain()
 
 
 class Trainer:
@@ -264,9 +278,13 @@ class Trainer:
         from .. import functional as mf
         if self._graph is not None and self.optimizer.layout_version != self._graph_layout:
             # optimizer state was replaced (load_state_dict with new tensors): the captured
-            # pointer table is stale -- rebuild it with one eager step, then re-capture
+            # pointer table is stale -- rebuild it with one eager step, then re-capture.
+            # Each replay leaves its gradients in place (the captured backward writes them,
+            # nothing zeroes them), so they are dropped first: the eager step's backward
+            # must not accumulate onto the last replay's gradients
             self._graph = None
             self._eager_calls = 1
+            self._zero_grad()
         if self._graph is None:
             if self._eager_calls < 2:  # warm-up: autotuning, workspaces, optimizer state, communicator
                 self._eager_calls += 1
@@ -281,7 +299,7 @@ class Trainer:
             if self.ddp is not None:
                 # no eager collective may still be listed with the process group's watchdog
                 # when the global-mode capture begins (quiesce_process_group)
-                quiesce_process_group()
+                quiesce_process_group(groups=(self.ddp.group,))
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g), mf.matmul_precision(self.precision):
                 self._static_loss = self._body(self._static)

@@ -47,6 +47,38 @@ def rng_fill(state_dict, seed=0, scale=0.05):
     return k
 
 
+def fanin_fill(state_dict, seed=7000, gains=None):
+    """Variance-preserving Gaussian weights (a well-conditioned network for bf16 parity):
+    entry k of the floating state_dict entries, in state_dict order, with r = rng_array(shape,
+    seed + k):
+        >= 2-D weights          gain / sqrt(fan_in) * r     (fan_in = elements per output row)
+        1-D ``*weight`` (norm)  1 + 0.1 * r
+        running_var             1 + 0.1 * |r|
+        other 1-D (bias, mean)  0.05 * r
+    gains: {name prefix: gain} (default 1).  Each layer then passes its input's scale on
+    (no activation grows or dies through depth), so bf16 operand rounding stays a
+    per-layer 2^-9 perturbation instead of being amplified by rank-deficient weights."""
+    k = 0
+    gains = gains or {}
+    with torch.no_grad():
+        for name, t in state_dict.items():
+            if not torch.is_floating_point(t):
+                continue
+            r = torch.from_numpy(rng_array(tuple(t.shape), seed + k)).double()
+            if t.dim() >= 2:
+                g = next((v for p, v in gains.items() if name.startswith(p)), 1.0)
+                vals = g / float(t[0].numel()) ** 0.5 * r
+            elif name.endswith("running_var"):
+                vals = 1.0 + 0.1 * r.abs()
+            elif name.endswith("weight"):
+                vals = 1.0 + 0.1 * r
+            else:
+                vals = 0.05 * r
+            t.copy_(vals.to(t.dtype))
+            k += 1
+    return k
+
+
 def rng_array(shape, seed=0):
     g = np.random.Generator(np.random.PCG64(seed))
     return g.standard_normal(size=shape).astype(np.float32)

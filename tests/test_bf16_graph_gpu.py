@@ -25,14 +25,8 @@ ACC_RTOL = 2e-6
 # (measured: outputs <= 1e-3, gradients <= 7e-2 -- BatchNorm affine gradients, sums of
 # dY x-hat over every pixel, carry the largest bf16 error)
 BF16_OUT_L2, BF16_GRAD_L2 = 1e-2, 1e-1
-# GPU bf16 vs the bf16-emulating fp64 oracle, per parameter gradient, beyond 20x the CPU fp32
-# emulation's own relative L2 error (test_depthformer_v8_480x640_bf16_vs_fp64_oracle)
-BF16_EMU_GRAD_L2 = 1e-2
-# a gradient whose bf16 rounding noise (bf16-emulating fp64 oracle vs the un-rounded fp64
-# oracle) is at least this fraction of its size is decided by where roundings fall, not by
-# the arithmetic: the GPU's distance from the exact (un-rounded) gradient is held to
-# BF16_NOISE_BALL x the emulation's own distance from it
-BF16_NOISE_DOMINATED, BF16_NOISE_BALL = 0.1, 3.0
+# configs[4] at size: the per-gradient draw rule of tests/bf16_criterion.py
+
 
 
 @pytest.fixture(scope="module")
@@ -219,57 +213,51 @@ def test_graph_replays_draw_new_dropout_masks(mf):
     assert len(set(losses[2:])) == 3
 
 
-@pytest.mark.parametrize("bn", ["train", "eval"])
-def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf, bn):
+def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
     """BASELINE configs[4] at its own size: Depthformer v8 with the benchmark's decoder (hidden
-    256, 4 heads, 256 bins, 256 aux tokens) at NYU 480x640, batch 2, train mode, under bf16
-    matmuls, against the oracle (oracle.depthformer, pinned to the reference by
+    256, 4 heads, 256 bins, 256 aux tokens) at NYU 480x640, batch 2, under bf16 matmuls,
+    against the oracle (oracle.depthformer, pinned to the reference by
     tests/golden/depthformer_v8.npz; restated B5 encoder) run with the SAME bf16 numerics
     (oracle.bf16emu: every conv / linear / matmul operand rounded to bf16, forward and
     backward, as mdemi_gemm_bf16 does).  o64 / o32 are that bf16-operand computation carried
-    out in fp64 / fp32 on the CPU.
+    out in fp64 / fp32 on the CPU; plain is the un-rounded fp64 model.
 
-    Outputs (depth, centres, the 8 attention maps):
-        max|gpu - o64| <= 20 x max|o32 - o64| + 1e-3 x max|o64|
-    (the fp32 full-size test's criterion).  EVERY parameter gradient, in relative L2:
-        ||gpu - o64|| / ||o64|| <= 20 x ||o32 - o64|| / ||o64|| + BF16_EMU_GRAD_L2
-    Relative L2, because bf16 rounding is discontinuous: an fp32-level difference upstream
-    moves an operand across a rounding boundary.  Gradients that are sums with heavy
-    cancellation are bf16 rounding residue: a value-projection bias's gradient is sum_i dO_i
-    (sum_j P~_ij) with P~ the bf16-rounded probabilities whose rows no longer sum to one; a key
-    projection's bias gradient is exactly zero by softmax's shift invariance.  For those the
-    emulation itself moves the gradient by more than its size (measured on the CPU, train-mode
-    BN: luna_layers.2.luna_attn.v1_proj.bias relative L2 3.49 between the bf16-emulating and the
-    un-rounded fp64 oracle).  So the noise n = ||o64 - plain64|| / ||o64|| is measured per
-    parameter, and a gradient with n >= BF16_NOISE_DOMINATED is held against the exact value:
-        ||gpu - plain64|| <= BF16_NOISE_BALL x ||o64 - plain64||
-    (the GPU's rounding moves it no farther from the exact gradient than 3x what the same
-    rounding does in the emulation; GPU and emulation round different fp32 values, so their
-    residues are independent draws and can differ from each other by more than either's
-    size -- measured 1.3-1.9 x n between builds that only reorder fp32 sums), while every other gradient
-    -- a wrong or missing term on a well-conditioned gradient -- takes the bound above.
+    The case is chosen so that bf16 rounding noise does not decide the verdict:
+    variance-preserving weights (oracle.weights.fanin_fill with bf16_criterion.
+    conditioned_gains) and BatchNorm on running statistics.  Fewer than 10 % of the
+    gradients are then bf16-noise-dominated (n = ||o64 - plain|| / ||o64|| >= 0.1; the
+    count is printed and asserted), and EVERY gradient is held to the draw rule of
+    tests/bf16_criterion.py:
+        ||gpu - o64|| <= 3 ||o32 - o64|| + 2e-3 ||o64||
+    (key-projection biases, exactly zero by softmax shift invariance, in size), which a 5 %
+    error on a Luna projection's gradient fails (tests/test_bf16_criterion.py).  Train-mode
+    BatchNorm over batch 2 is not such a case -- there the median gradient's bf16 noise is
+    0.9 of its size, so no end-to-end bound discriminates; its bf16 GEMMs are held one by one
+    instead (test_every_bf16_gemm_of_the_configs4_step_is_exact).
 
-    What bf16 itself costs against the fp32 model is reported beside it: depth and centres
-    are held to BF16_OUT_L2 relative L2 against the un-rounded fp64 oracle.
-    depthformer_v8.py:46-75, decoder_v8.py:97-171."""
-    import test_models_gpu as tm
-    from mdemi.model.Depthformer import DepthformerV8
+    Outputs (depth, centres, the 8 attention maps): max|gpu - o64| <= 20 x max|o32 - o64| +
+    1e-3 x max|o64|; depth and centres within BF16_OUT_L2 relative L2 of plain (what bf16
+    costs against the fp32 model).  depthformer_v8.py:46-75, decoder_v8.py:97-171,
+    luna_layer.py:181-259."""
     import contextlib
 
+    import bf16_criterion as crit
+    from mdemi.model.Depthformer import DepthformerV8
     from oracle import bf16emu, bnmode
     from oracle import depthformer as odf
-    from oracle.weights import rng_array
+    from oracle.weights import fanin_fill, rng_array
 
     torch.set_num_threads(16)
     opt = {"hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256, "img_size": [480, 640],
            "attn_drop_prob": 0.0, "drop_prob": 0.0}
     m = DepthformerV8.build(opt, 1e-3, 10.0)
-    sd = tm._filled_state(m, 0.53, 0.03)
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    fanin_fill(sd, gains=crit.conditioned_gains())
+    m.load_state_dict(sd)
     m = m.to(DEV).train()
-    if bn == "eval":  # BatchNorm on running statistics (everything else in train mode)
-        for mod in m.modules():
-            if isinstance(mod, torch.nn.BatchNorm2d):
-                mod.eval()
+    for mod in m.modules():  # BatchNorm on running statistics (everything else in train mode)
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.eval()
     img = torch.from_numpy(rng_array((2, 3, 480, 640), 84))
     with mf.matmul_precision("bf16"):
         depth, centers, attn = m(img.float().to(DEV))
@@ -282,61 +270,131 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf, bn):
     def oracle(dtype, emulate):
         P = {k: (v.detach().to(dtype).clone().requires_grad_(True) if torch.is_floating_point(v) else v)
              for k, v in sd.items()}
-        ctx = bf16emu.enabled() if emulate else contextlib.nullcontext()
-        with ctx, (bnmode.eval_bn() if bn == "eval" else contextlib.nullcontext()):
+        with (bf16emu.enabled() if emulate else contextlib.nullcontext()), bnmode.eval_bn():
             d, c, a = odf.depthformer_v8_full(P, img.to(dtype), opt, 1e-3, 10.0)
             (d * dy.to(dtype)).sum().backward()
-        return [t.detach() for t in [d, c] + list(a)], P
+        return [t.detach() for t in [d, c] + list(a)], {k: p.grad for k, p in P.items()
+                                                       if torch.is_tensor(p) and p.grad is not None}
 
-    o64, P64 = oracle(torch.float64, True)
-    o32, P32 = oracle(torch.float32, True)
-    plain, Pplain = oracle(torch.float64, False)
-
-    def within(name, got, r64, r32):
-        e_gpu = (got.detach().double().cpu() - r64).abs().max().item()
-        e_cpu = (r32.double() - r64).abs().max().item()
-        mag = r64.abs().max().item()
-        assert e_gpu <= 20.0 * e_cpu + 1e-3 * mag + 1e-12, (name, e_gpu, e_cpu, mag)
-        return e_gpu / (mag + 1e-300)
+    o64, G64 = oracle(torch.float64, True)
+    o32, G32 = oracle(torch.float32, True)
+    plain, Gplain = oracle(torch.float64, False)
 
     worst = []
     for k, g, r64, r32 in zip(names, gpu_out, o64, o32):
-        worst.append((within(k, g, r64, r32), k))
-    n, diag = 0, []
-    for k, p in m.named_parameters():
-        r64, r32 = P64[k].grad, P32[k].grad
-        n += 1
-        if r64 is None:
-            assert p.grad is None or p.grad.abs().max().item() == 0, k
-            continue
-        g = p.grad.detach().double().cpu()
-        l2 = lambda a: torch.linalg.norm(a).item()  # noqa: E731
-        ref = l2(r64) + 1e-300
-        diag.append((l2(g - r64) / ref, l2(r32.double() - r64) / ref, l2(Pplain[k].grad - r64) / ref,
-                     l2(r64) / r64.numel() ** 0.5, k, l2(g - Pplain[k].grad) / ref))
-    assert n == len(list(m.parameters()))
-    for d in sorted(diag, reverse=True)[:12]:
-        print(f"  grad rel-L2 gpu {d[0]:.3e}  cpu32 {d[1]:.3e}  bf16 noise {d[2]:.3e}  rms {d[3]:.3e}  {d[4]}")
-    tight = [d for d in diag if d[0] <= 20.0 * d[1] + BF16_EMU_GRAD_L2]
-    bad = [(k, e_gpu, e_cpu, noise, g_plain) for e_gpu, e_cpu, noise, _, k, g_plain in diag
-           if e_gpu > 20.0 * e_cpu + BF16_EMU_GRAD_L2 and
-           not (noise >= BF16_NOISE_DOMINATED and g_plain <= BF16_NOISE_BALL * noise)]
-    noisy = [d for d in diag if d[2] >= BF16_NOISE_DOMINATED]
-    ball = [d for d in diag if d not in tight]
-    for d in sorted(ball, key=lambda d: -d[5] / max(d[2], 1e-300))[:8]:
-        print(f"  noise-ball: |gpu-exact| {d[5]:.3e}  |emu-exact| {d[2]:.3e}  ratio {d[5] / max(d[2], 1e-300):.2f}  {d[4]}")
-    print(f"  {len(noisy)} of {len(diag)} gradients bf16-noise-dominated; {len(tight)} within the tight bound, "
-          f"{len(ball) - len(bad)} by the noise ball; beyond the bounds: {bad}")
-    assert not bad, bad
+        e_gpu = (g.detach().double().cpu() - r64).abs().max().item()
+        e_cpu = (r32.double() - r64).abs().max().item()
+        mag = r64.abs().max().item()
+        assert e_gpu <= 20.0 * e_cpu + 1e-3 * mag + 1e-12, (k, e_gpu, e_cpu, mag)
+        worst.append((e_gpu / (mag + 1e-300), k))
+    params = dict(m.named_parameters())
+    assert set(G64) == set(params), set(params) ^ set(G64)
+    gpu = {k: p.grad.detach().double().cpu() for k, p in params.items()}
+    r = crit.judge(gpu, G64, G32, Gplain)
+    for ratio, k, err, bound, n in r["rows"][:10]:
+        print(f"  {k:60s} |gpu-o64| {err:.3e} bound {bound:.3e} ({ratio:.2f} of it)  bf16 noise {n:.2e}")
+    luna = [(k, err / torch.linalg.norm(G64[k]).item(), bound / torch.linalg.norm(G64[k]).item())
+            for _, k, err, bound, _ in r["rows"]
+            if "luna_attn" in k and k.endswith("weight") and any(f".{x}_proj." in k for x in ("v1", "o1", "v2", "o2"))]
+    print(f"  Luna value/output projection weights: relative bound {min(b for _, _, b in luna):.2%}.."
+          f"{max(b for _, _, b in luna):.2%}, GPU at {min(e for _, e, _ in luna):.2%}..{max(e for _, e, _ in luna):.2%}")
+    print(f"configs[4] bf16, 480x640, eval-BN conditioned case: {len(r['noisy'])} of {r['checked']} gradients "
+          f"bf16-noise-dominated; {r['checked'] - len(r['bad'])} within the draw bound; beyond it: {r['bad']}")
+    assert r["checked"] == len(params)
+    assert len(r["noisy"]) < crit.MAX_NOISY_FRACTION * r["checked"], r["noisy"]
+    assert not r["bad"], r["bad"]
 
-    def rel_l2(a, r):
-        a, r = a.detach().double().cpu().reshape(-1), r.reshape(-1)
-        return (torch.linalg.norm(a - r) / torch.linalg.norm(r)).item()
+    def rel_l2(a, ref):
+        a, ref = a.detach().double().cpu().reshape(-1), ref.reshape(-1)
+        return (torch.linalg.norm(a - ref) / torch.linalg.norm(ref)).item()
 
-    cost = {k: rel_l2(g, r) for k, g, r in zip(names, gpu_out, plain)}
+    cost = {k: rel_l2(g, ref) for k, g, ref in zip(names, gpu_out, plain)}
     print(f"configs[4] bf16: worst max-error / magnitude vs the bf16-emulating fp64 oracle "
           f"{sorted(worst, reverse=True)[:5]}; relative L2 vs the fp32-numerics fp64 oracle {cost}")
     assert cost["depth"] <= BF16_OUT_L2 and cost["centers"] <= BF16_OUT_L2, cost
+
+
+def test_every_bf16_gemm_of_the_configs4_step_is_exact(mf):
+    """Every bf16 GEMM of a configs[4] train step -- Depthformer v8 (hidden 256, 256 bins,
+    256 aux tokens) at NYU 480x640, batch 2, BatchNorm in train mode, forward + backward --
+    is re-run as an exact-product fp32 GEMM (v_mfma_f32_32x32x2_f32) on its operands rounded
+    to bf16 (RNE), with the same descriptor and epilogue.  bf16 x bf16 products are exact in
+    fp32, so the two may differ only by fp32 accumulation order:
+        max|bf16 - ref| <= 2 x ACC_RTOL x max_ij sum_k |a_ik b_kj|   (epilogue Lipschitz <= 1.2)
+    with the abs-product computed by the same fp32 GEMM on |A|, |B| without the epilogue.
+    GELU-on-load operands (a_op / b_op) round GELU(x) computed on the device, whose last bit
+    may differ from torch's: those calls are held to the operand-rounding bound 2^-8 x
+    abs-product.  This is the per-GEMM form of the whole-step bf16 parity (tools/bf16_audit.py
+    promoted to a test); the train-mode step's end-to-end gradients are too noise-dominated
+    at batch 2 for an end-to-end bound (test_depthformer_v8_480x640_bf16_vs_fp64_oracle)."""
+    import bf16_criterion as crit
+    from mdemi import _lib as L
+    from mdemi.model.Depthformer import DepthformerV8
+    from oracle.weights import fanin_fill, rng_array
+
+    opt = {"hidden_dim": 256, "num_heads": 4, "num_bins": 256, "num_aux": 256, "img_size": [480, 640],
+           "attn_drop_prob": 0.0, "drop_prob": 0.0}
+    m = DepthformerV8.build(opt, 1e-3, 10.0)
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    fanin_fill(sd, gains=crit.conditioned_gains())
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    img = torch.from_numpy(rng_array((2, 3, 480, 640), 84)).float().to(DEV)
+    orig = mf.gemm
+    stats = {"calls": 0, "op_calls": 0, "worst": (0.0, None)}
+    bad = []
+    epilogue_keys = ("bias", "aux", "residual", "preact", "rowsum_a")
+
+    def audited(A, B, C, M, N, K, **kw):
+        if mf.get_matmul_precision() != "bf16":
+            return orig(A, B, C, M, N, K, **kw)
+        before = C.clone()
+        saved = {k: kw[k].clone() for k in ("aux", "preact", "rowsum_a") if kw.get(k) is not None}
+        out = orig(A, B, C, M, N, K, **kw)
+        got = C.clone()
+        after = {k: kw[k].clone() for k in saved}
+        a_op, b_op = kw.get("a_op", 0), kw.get("b_op", 0)
+        Ar = (torch.nn.functional.gelu(A) if a_op else A).to(torch.bfloat16).float()
+        Br = (torch.nn.functional.gelu(B) if b_op else B).to(torch.bfloat16).float()
+        kw_ref = dict(kw, a_op=L.OP_NONE, b_op=L.OP_NONE, rowsum_a=None)
+        C.copy_(before)
+        for k, v in saved.items():
+            kw[k].copy_(v)
+        with mf.matmul_precision("fp32"):
+            orig(Ar, Br, C, M, N, K, **kw_ref)
+            ref = C.clone()
+            kw_abs = dict(kw_ref, alpha=abs(kw.get("alpha", 1.0)), beta=0.0, bias=None, bias_mode=L.BIAS_NONE,
+                          act=L.ACT_NONE, aux=None, residual=None, preact=None)
+            C.zero_()
+            orig(Ar.abs(), Br.abs(), C, M, N, K, **kw_abs)
+            absprod = C.abs().max().item()
+        C.copy_(got)  # the step continues with the bf16 results
+        for k, v in after.items():
+            kw[k].copy_(v)
+        torch.cuda.synchronize()
+        err = (got - ref).abs().max().item()
+        lim = (2.0 ** -8 if (a_op or b_op) else 2.0 * ACC_RTOL) * absprod + 1e-30
+        stats["calls"] += 1
+        stats["op_calls"] += int(bool(a_op or b_op))
+        if err / lim > stats["worst"][0]:
+            stats["worst"] = (err / lim, (M, N, K, kw.get("a_layout"), kw.get("b_layout")))
+        if err > lim:
+            bad.append((M, N, K, kw.get("a_layout"), kw.get("b_layout"), err, lim))
+        return out
+
+    mf.gemm = audited
+    try:
+        with mf.matmul_precision("bf16"):
+            depth, centers, attn = m(img)
+            dy = torch.from_numpy(rng_array(tuple(depth.shape), 85)).float().to(DEV)
+            (depth * dy).sum().backward()
+        torch.cuda.synchronize()
+    finally:
+        mf.gemm = orig
+    print(f"configs[4] step: {stats['calls']} bf16 GEMM calls audited ({stats['op_calls']} with GELU-on-load), "
+          f"worst at {stats['worst'][0]:.3f} of its bound {stats['worst'][1]}; beyond: {bad[:10]}")
+    assert stats["calls"] >= 400
+    assert not bad, bad
 
 
 def test_bf16_variants_bit_identical(mf):

@@ -186,6 +186,8 @@ def test_oda2_large_kitti_train_step(lib):
            "eval": {"max_depth_eval": 80, "min_depth_eval": 0.001}}
     torch.manual_seed(0)
     tr = build_from_config(copy.deepcopy(opt), device=DEV, steps_per_epoch=10)
+    reducer = tr.model.decoder.reducer
+    reducer.validate_indices = True  # count what the kernels' index clamp would hide
     g = torch.Generator().manual_seed(5)
     img = torch.randn(2, 3, 352, 704, generator=g).to(DEV)
     gt = (torch.rand(2, 1, 352, 704, generator=g) * 79 + 1).to(DEV)
@@ -195,6 +197,9 @@ def test_oda2_large_kitti_train_step(lib):
     assert torch.isfinite(loss).item()
     moved = sum(int(not torch.equal(before[k], p.detach())) for k, p in tr.model.named_parameters())
     assert moved == len(before), (moved, len(before))
+    # no depth index left [0, num_emb) on this step: the reference's F.embedding would have
+    # accepted every one, so the clamp changed nothing
+    assert int(reducer.clamped_indices.item()) == 0
     tr.model.eval()
     with torch.no_grad():
         out, outs, attn = tr.model(torch.randn(1, 3, 352, 1216, device=DEV))

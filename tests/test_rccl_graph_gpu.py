@@ -125,6 +125,120 @@ def test_optimizer_resume_after_capture(rccl):
         assert torch.equal(a, b), k
 
 
+def test_layout_change_after_capture_drops_replay_gradients(mf_lib):
+    """a single-process captured step leaves its gradients in place after each
+    replay.  When a load_state_dict changes the optimizer's layout (here: one parameter's
+    state dropped, so its moments restart), the trainer runs one eager step before it
+    re-captures -- that step must not accumulate onto the last replay's gradients.  Eager and
+    captured trainers, given the same state dict, agree bit for bit over the steps after it
+    (eager re-warm-up, re-capture, replay)."""
+    from mdemi.train import build_from_config
+    opt = _dfv8_opt(1)
+    torch.manual_seed(0)
+    eager = build_from_config(copy.deepcopy(opt), device=DEV, steps_per_epoch=20, precision="bf16")
+    torch.manual_seed(0)
+    graph = build_from_config(copy.deepcopy(opt), device=DEV, steps_per_epoch=20, precision="bf16", graph=True)
+    graph.model.load_state_dict(eager.model.state_dict())
+    for s in range(3):
+        b = [_batch(400 + s)]
+        eager.step(b)
+        graph.step(b)
+    assert graph._graph is not None
+    v0 = graph.optimizer.layout_version
+    sd = eager.optimizer.state_dict()
+    dropped = sorted(sd["state"])[len(sd["state"]) // 2]
+    sd = {"state": {i: {k: v.clone() for k, v in st.items()} for i, st in sd["state"].items() if i != dropped},
+          "param_groups": copy.deepcopy(sd["param_groups"])}
+    eager.optimizer.load_state_dict(copy.deepcopy(sd))
+    graph.optimizer.load_state_dict(copy.deepcopy(sd))
+    assert graph.optimizer.layout_version != v0  # the stale-graph path is the one under test
+    le = [eager.step([_batch(500 + s)]).item() for s in range(3)]
+    lg = [graph.step([_batch(500 + s)]).item() for s in range(3)]
+    assert graph._graph is not None and graph._graph_layout == graph.optimizer.layout_version
+    assert le == lg, (le, lg)
+    for (k, a), b in zip(eager.model.state_dict().items(), graph.model.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
+@pytest.fixture(scope="module")
+def mf_lib():
+    from mdemi import _lib
+    _lib.load()
+
+
+def _large07_kitti_opt():
+    """json/kitti/newcrfs/newcrfs_github_eval.json's train keys (bench.py _NEWCRFS_KITTI)."""
+    return {"model": {"name": "newcrfs"}, "loss": {"alpha": 10.0, "beta": 0.15, "per_image": False},
+            "dataset": {"data_type": "KITTI"}, "dataloader": {"batch_size": 2},
+            "optimizer": {"lr": 2e-5, "weight_decay": 0.0},
+            "scheduler": {"name": "onecycle", "pct_start": 0.3, "div_factor": 25, "final_div_factor": 100},
+            "train": {"epoch": 25, "num_accum": 1, "grad_norm": 0.1},
+            "eval": {"max_depth_eval": 80, "min_depth_eval": 0.001, "garg_crop": True, "eigen_crop": False}}
+
+
+def test_newcrfs_large07_kitti_ddp_rccl_matches_single_process(rccl):
+    """BASELINE configs[3]'s data-parallel path on RCCL: NeW-CRFs large07 (270 M parameters,
+    1.08 GB of fp32 gradients) at KITTI 352x1216, batch 2, through GradAllReduce with the
+    default 64 MB buckets on the world-1 "nccl" group.  Three DDP train steps (forward, SILog,
+    backward whose hooks launch every bucket's RCCL all-reduce as it fills, finish(), clipped
+    AdamW, OneCycle) equal three single-process steps bit for bit: losses, every weight, the
+    optimizer moments and step counters; the buckets launch in index order.
+    Reference: utils/dist_utils.py:31-64, utils/common_utils.py:20-21,
+    model/NewCRFs/NewCRFDepth.py:123-148."""
+    from mdemi.train import build_from_config
+    opt = _large07_kitti_opt()
+    torch.manual_seed(0)
+    # drop_path 0: DropPath draws its per-sample masks from the GPU generator, which the two
+    # trainers would advance alternately
+    single = build_from_config(copy.deepcopy(opt), device=DEV, steps_per_epoch=100, drop_path=0.0)
+    torch.manual_seed(0)
+    ddp = build_from_config(copy.deepcopy(opt), device=DEV, steps_per_epoch=100, ddp=True, drop_path=0.0)
+    ddp.model.load_state_dict(single.model.state_dict())
+    assert single.ddp is None and ddp.ddp is not None
+    grad_bytes = sum(ddp.ddp.bucket_bytes)
+    assert grad_bytes >= 1.08e9 and len(ddp.ddp.buckets) >= 16, (grad_bytes, len(ddp.ddp.buckets))
+
+    def batch(seed):  # SURVEY §8d KITTI: U(1, 80) depth at a Bernoulli(0.15) LiDAR-like mask
+        g = torch.Generator().manual_seed(seed)
+        img = torch.randn(2, 3, 352, 1216, generator=g)
+        gt = (torch.rand(2, 1, 352, 1216, generator=g) * 79.0 + 1.0) * (torch.rand(2, 1, 352, 1216, generator=g) < 0.15)
+        return img.to(DEV), gt.to(DEV)
+
+    ls, ld = [], []
+    for s in range(3):
+        b = [batch(600 + s)]
+        ls.append(single.step(b).item())
+        ld.append(ddp.step(b).item())
+        assert ddp.ddp.last_launch_order == list(range(len(ddp.ddp.buckets)))
+    assert ls == ld, (ls, ld)
+    for (k, a), b in zip(single.model.state_dict().items(), ddp.model.state_dict().values()):
+        assert torch.equal(a, b), k
+    so, do = single.optimizer.state_dict(), ddp.optimizer.state_dict()
+    assert so["state"].keys() == do["state"].keys()
+    for i in so["state"]:
+        for k in ("exp_avg", "exp_avg_sq", "step"):
+            a, b = so["state"][i][k], do["state"][i][k]
+            assert (torch.equal(a, b) if torch.is_tensor(a) else a == b), (i, k)
+    print(f"large07 KITTI DDP on RCCL: {len(ddp.ddp.buckets)} buckets, {grad_bytes / 1e9:.3f} GB, losses {ld}")
+
+
+def test_quiesce_drains_every_nccl_group(rccl):
+    """the capture precondition drains each RCCL group the captured step uses, not
+    only the default one (GradAllReduce(group=...))."""
+    from mdemi.train.builder import quiesce_process_group
+    sub = dist.new_group([0], backend="nccl")
+    t = torch.ones(1 << 16, device=DEV)
+    works = [dist.all_reduce(t, group=sub, async_op=True) for _ in range(4)]
+    quiesce_process_group(works, groups=(sub,))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        dist.all_reduce(t, group=sub)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(t, torch.ones_like(t))
+    dist.destroy_process_group(sub)
+
+
 def test_capture_right_after_collectives(rccl):
     """a global-mode capture begun right after eager collectives must not race the
     process group's watchdog.  quiesce_process_group waits on the Works, then on
