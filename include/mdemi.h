@@ -144,6 +144,23 @@ int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream);
  * as mdemi_gemm_f32 (swin_transformer.py:18-20,104,106,259; newcrf_layers.py:
  * 16-20,102,104,384,389; uper_crf_head.py:38-44,341-348; ...). */
 int mdemi_gemm_f32e(const mdemi_gemm_desc* d, void* stream);
+/* bf16 storage path of precision "bf16" (BASELINE configs[4]): the same contract as
+ * mdemi_gemm_bf16 with the operands given as bf16 tensors (a16, b16: 16-bit RNE copies of
+ * A and B, same layouts, leading dimensions and strides in elements) DMA'd straight into
+ * LDS, so an activation or weight stored in bf16 is read at 2 B per element with no
+ * conversion; results are bit-identical to mdemi_gemm_bf16 on the fp32 tensors whose RNE
+ * bf16 a16/b16 are.  c16 (optional, may be NULL): a bf16 (RNE) copy of the final output,
+ * C's layout, written by the same epilogue (the bf16 operand of a later GEMM).  Layouts
+ * the bf16 loaders cannot stage (K / extent / C not a multiple of 8, a load-time op,
+ * rowsum_a) fall back to mdemi_gemm_bf16 on d->A / d->B, which must then be given.
+ * Replaces the autocast bf16 conv/linear/bmm of model/Depthformer/layer_utils.py:6-34,
+ * luna_layer.py:181-259, decoder_v8.py:97-171. */
+int mdemi_gemm_bf16x(const mdemi_gemm_desc* d, const void* a16, const void* b16, void* c16, void* stream);
+/* 1 when mdemi_gemm_bf16x would take the bf16-operand path for this descriptor. */
+int mdemi_gemm_bf16x_supported(const mdemi_gemm_desc* d, const void* a16, const void* b16);
+/* tuning hook of the bf16-operand family: 0 = 128-row tile, 1 = 256-row tile, -1 = per-shape
+ * autotune (default; bit-identical). */
+int mdemi_gemm_set_variant_b16(int32_t variant);
 /* tuning hook: pipelining variant (0..5, see gemm_f32.hip; -1 = time the
  * candidates once per distinct shape and cache the winner, the default -- all
  * variants produce bit-identical results) and tile raster (group_m > 0:

@@ -49,6 +49,7 @@ struct GemmParams {
   int tiles_m1, m_split;
   int* tile_cnt;  // non-null: the last-arriving split of a tile combines the slabs (no reduce launch)
   float* rowsum_out;  // with tile_cnt and split row-sum partials: the last arriver writes the sums here
+  void* c16;  // optional bf16 copy (RNE) of the final output, C's layout: the bf16 operand of a later GEMM
 };
 
 // One thread's 4 bias-gradient row sums (rows i..i+3) of a K piece: plain stores, or
@@ -398,7 +399,9 @@ __device__ __forceinline__ GemmJob job_of(const GemmParams& p) {
 constexpr int GEMM_F32 = 0;   // exact-product fp32 MFMA (gemm_f32.hip)
 constexpr int GEMM_BF16 = 1;  // bf16 operands, fp32 accumulate (gemm_mfma16.hip, NP = 1)
 constexpr int GEMM_F32E = 2;  // fp32 as three bf16 planes, six products (gemm_mfma16.hip, NP = 3)
+constexpr int GEMM_B16 = 3;   // bf16 operands in HBM, direct-to-LDS (gemm_b16_kernel.h); numerics of GEMM_BF16
 
 void (*pick_kernel_m16(int al, int bl, int aop, int bop, int np, int v))(GemmParams);
+void (*pick_kernel_b16(int al, int bl, int v))(GemmParams);
 
 }  // namespace mdemi

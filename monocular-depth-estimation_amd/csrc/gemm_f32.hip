@@ -111,6 +111,7 @@ static bool env_on(const char* name) {
 static bool g_tail_split = env_on("MDEMI_GEMM_TAIL_SPLIT");
 static bool g_inline_reduce = env_on("MDEMI_GEMM_INLINE_REDUCE");
 static int g_variant_m16 = -1;  // 16-bit family (bf16 / split fp32): 0 two LDS buffers, 1 one
+static int g_variant_b16 = -1;  // bf16-operand family: 0 128-row tile, 1 256-row tile
 static int g_group_m = 8;
 
 KernelFn f32_pick_part0(int al, int bl, int aop, int bop, int v);
@@ -134,11 +135,12 @@ static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
 }
 
 static int variant_bk(int v, int mode) {
-  if (mode != GEMM_F32) return 32;
+  if (mode != GEMM_F32) return 32;  // the 16-bit and bf16-operand families: BK 32
   if (v >= 8) return (v == 8 || v == 10) ? 32 : 16;
   return (v >= 3 && v != 7) ? 32 : 16;
 }
 static int variant_rows(int v, int mode) {
+  if (mode == GEMM_B16) return v == 1 ? 2 * GBM : GBM;
   return (mode != GEMM_F32 ? (v == 2 || v == 4) : (v == 6 || v == 7 || v == 9 || v == 10)) ? 2 * GBM : GBM;
 }
 // the direct-to-LDS variants need dense operands that load as whole 16-B quads and no
@@ -263,6 +265,7 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
   p.m_split = (tp.split > 1 && p.split > 1) ? tp.m_split : 0;
   p.tile_cnt = nullptr;
   p.rowsum_out = nullptr;
+  p.c16 = nullptr;
   // vector loads need every row start 16-B aligned and whole quads in range
   // (KCONTIG: K % 4; MNCONTIG: the row/column extent % 4)
   p.a_vec = al16(d->A) && (d->lda % 4 == 0) && (d->a_bstride % 4 == 0) && (p.a_bs2 % 4 == 0) &&
@@ -327,16 +330,22 @@ static size_t colsum_combine_bytes(const mdemi_gemm_desc* d, const GemmParams& p
   return colsum_combine(d, p) ? colsum_ws_bytes(p.split, (int64_t)d->M * d->N) : 0;
 }
 
-static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mode) {
+// bf16 operands / output of mdemi_gemm_bf16x (null for the fp32-operand entry points)
+struct B16Ext {
+  const void* a16; const void* b16; void* c16;
+};
+
+static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mode, const B16Ext* ext = nullptr) {
   if (mode == GEMM_F32E && variant >= 3) variant = 0;  // the bf16-image variants hold one bf16 plane
   if (mode == GEMM_F32 && variant >= 8) {  // a forced direct-to-LDS variant on an operand it cannot stage
     GemmParams q;
     fill_params(d, q, variant, mode);
     if (!glds_ok(d, q)) variant = 0;
   }
-  KernelFn fn = mode == GEMM_F32 ? pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant)
-                                 : pick_kernel_m16(d->a_layout, d->b_layout, d->a_op, d->b_op,
-                                                   mode == GEMM_BF16 ? 1 : 3, variant);
+  KernelFn fn = mode == GEMM_F32   ? pick_kernel(d->a_layout, d->b_layout, d->a_op, d->b_op, variant)
+                : mode == GEMM_B16 ? pick_kernel_b16(d->a_layout, d->b_layout, variant)
+                                   : pick_kernel_m16(d->a_layout, d->b_layout, d->a_op, d->b_op,
+                                                     mode == GEMM_BF16 ? 1 : 3, variant);
   if (!fn) {
     set_error("gemm: unsupported layout/op combination a=%d/%d b=%d/%d", d->a_layout, d->a_op, d->b_layout,
               d->b_op);
@@ -344,6 +353,13 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mod
   }
   GemmParams p;
   fill_params(d, p, variant, mode);
+  if (ext) {
+    p.c16 = ext->c16;
+    if (mode == GEMM_B16) {  // the kernel reads the bf16 tensors through the A/B slots
+      p.A = reinterpret_cast<const float*>(ext->a16);
+      p.B = reinterpret_cast<const float*>(ext->b16);
+    }
+  }
   float* rowsum_part = nullptr;
   if (p.split > 1) {
     const size_t need = slab_bytes(d, p) + rowsum_bytes(d, p) + colsum_combine_bytes(d, p);
@@ -381,7 +397,7 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mod
                          rowsum_part ? d->rowsum_a : (float*)nullptr);
     }
   }
-  return check_launch(mode == GEMM_BF16 ? "gemm_bf16" : mode == GEMM_F32E ? "gemm_f32e" : "gemm_f32");
+  return check_launch(mode == GEMM_BF16 ? "gemm_bf16" : mode == GEMM_F32E ? "gemm_f32e" : mode == GEMM_B16 ? "gemm_bf16x" : "gemm_f32");
 }
 
 struct TuneKey {
@@ -405,8 +421,12 @@ static bool tunable(const mdemi_gemm_desc* d, hipStream_t st) {
   return true;
 }
 
-static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
-  if (mode != GEMM_F32 ? g_variant_m16 >= 0 : g_variant >= 0) return mode != GEMM_F32 ? g_variant_m16 : g_variant;
+static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode, const B16Ext* ext = nullptr) {
+  if (mode == GEMM_B16) {
+    if (g_variant_b16 >= 0) return g_variant_b16;
+  } else if (mode != GEMM_F32 ? g_variant_m16 >= 0 : g_variant >= 0) {
+    return mode != GEMM_F32 ? g_variant_m16 : g_variant;
+  }
   const TuneKey key{d->a_layout, d->b_layout, d->a_op, d->b_op, d->M, d->N, d->K, d->batch, d->split_k, mode};
   {
     std::lock_guard<std::mutex> lk(g_tune_mu);
@@ -414,10 +434,11 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
     if (it != g_tuned.end()) return it->second;
   }
   if (!tunable(d, st)) return 0;
+  if (ext && ext->c16 && (ext->c16 == ext->a16 || ext->c16 == ext->b16)) return 0;
   static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11};
   static const int cands_m16[] = {0, 1, 2, 3, 4};
   const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
-  int ncand = mode == GEMM_BF16 ? 5 : mode == GEMM_F32E ? 3 : 11;
+  int ncand = mode == GEMM_BF16 ? 5 : mode == GEMM_F32E ? 3 : mode == GEMM_B16 ? 2 : 11;
   if (mode == GEMM_F32) {
     GemmParams q;
     fill_params(d, q, 0, mode);
@@ -429,9 +450,9 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode) {
   float best_ms = 1e30f;
   for (int ci = 0; ci < ncand; ++ci) {
     const int v = cands[ci];
-    if (launch(d, v, st, mode) != MDEMI_OK) continue;  // warm (and validate)
+    if (launch(d, v, st, mode, ext) != MDEMI_OK) continue;  // warm (and validate)
     (void)hipEventRecord(e0, st);
-    for (int r = 0; r < 3; ++r) launch(d, v, st, mode);
+    for (int r = 0; r < 3; ++r) launch(d, v, st, mode, ext);
     (void)hipEventRecord(e1, st);
     float ms = 0.f;
     if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
@@ -459,6 +480,53 @@ static int gemm_entry(const mdemi_gemm_desc* d, void* stream, int mode) {
   return launch(d, choose_variant(d, st, mode), st, mode);
 }
 
+// bf16-operand path: both operands bf16 in HBM and a layout the DMA loaders stage (16-B
+// quads of 8 bf16: k-contiguous K % 8, m/n-contiguous extent % 8, implicit-im2col C % 8,
+// leading dimensions and batch strides % 8, 16-B aligned bases, no load-time op, no
+// bias-gradient row sums -- those are summed from the unrounded fp32 operand)
+static bool al16v(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static bool b16_ok(const mdemi_gemm_desc* d, const B16Ext& e) {
+  if (!e.a16 || !e.b16 || !al16v(e.a16) || !al16v(e.b16)) return false;
+  if (d->a_op != MDEMI_OP_NONE || d->b_op != MDEMI_OP_NONE || d->rowsum_a) return false;
+  if (d->a_layout == MDEMI_L_CONV && d->b_layout == MDEMI_L_CONV) return false;
+  auto operand = [&](int layout, int64_t ld, int64_t bs, int64_t bs2, int64_t extent) {
+    if (layout == MDEMI_L_CONV) {
+      const mdemi_conv_geom& g = d->conv;
+      return g.c % 8 == 0 && (int64_t)g.n * g.h * g.w * g.c * 2 < ((int64_t)1 << 31);
+    }
+    if (ld % 8 || bs % 8 || bs2 % 8) return false;
+    return layout == MDEMI_L_KCONTIG ? d->K % 8 == 0 : extent % 8 == 0;
+  };
+  const int64_t ai = d->batch_inner > 1 ? d->a_bstride_inner : 0, bi = d->batch_inner > 1 ? d->b_bstride_inner : 0;
+  return operand(d->a_layout, d->lda, d->a_bstride, ai, d->M) && operand(d->b_layout, d->ldb, d->b_bstride, bi, d->N);
+}
+
+extern "C" int mdemi_gemm_bf16x(const mdemi_gemm_desc* d, const void* a16, const void* b16, void* c16, void* stream) {
+  MDEMI_REQUIRE(d, "gemm: null descriptor");
+  const B16Ext e{a16, b16, c16};
+  hipStream_t st = (hipStream_t)stream;
+  if (b16_ok(d, e)) {
+    mdemi_gemm_desc v = *d;  // validate() checks the fp32 operand slots; the bf16 ones stand in
+    v.A = (const float*)a16;
+    v.B = (const float*)b16;
+    int rc = validate(&v);
+    if (rc) return rc;
+    return launch(d, choose_variant(d, st, GEMM_B16, &e), st, GEMM_B16, &e);
+  }
+  // a layout the bf16 loaders cannot stage: the m16 family on the fp32 operands (the same
+  // bf16 products, bit for bit)
+  MDEMI_REQUIRE(d->A && d->B, "gemm_bf16x: no bf16 path for this layout (a=%d b=%d) and no fp32 operands given",
+                d->a_layout, d->b_layout);
+  int rc = validate(d);
+  if (rc) return rc;
+  const B16Ext f{nullptr, nullptr, c16};
+  return launch(d, choose_variant(d, st, GEMM_BF16, &f), st, GEMM_BF16, &f);
+}
+
+extern "C" int mdemi_gemm_bf16x_supported(const mdemi_gemm_desc* d, const void* a16, const void* b16) {
+  return d && b16_ok(d, B16Ext{a16, b16, nullptr}) ? 1 : 0;
+}
+
 extern "C" int mdemi_gemm_f32(const mdemi_gemm_desc* d, void* stream) { return gemm_entry(d, stream, GEMM_F32); }
 extern "C" int mdemi_gemm_bf16(const mdemi_gemm_desc* d, void* stream) { return gemm_entry(d, stream, GEMM_BF16); }
 extern "C" int mdemi_gemm_f32e(const mdemi_gemm_desc* d, void* stream) { return gemm_entry(d, stream, GEMM_F32E); }
@@ -483,5 +551,11 @@ extern "C" int mdemi_gemm_set_options(int32_t tail_split, int32_t inline_reduce)
 extern "C" int mdemi_gemm_set_variant_m16(int32_t variant) {
   MDEMI_REQUIRE(variant >= -1 && variant < 5, "gemm_set_variant_m16: bad variant");
   g_variant_m16 = variant;
+  return MDEMI_OK;
+}
+
+extern "C" int mdemi_gemm_set_variant_b16(int32_t variant) {
+  MDEMI_REQUIRE(variant >= -1 && variant < 2, "gemm_set_variant_b16: bad variant");
+  g_variant_b16 = variant;
   return MDEMI_OK;
 }

@@ -117,10 +117,13 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
          res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0, rowsum_a=None,
-         a_off=0, b_off=0, c_off=0, inner=None, row_scale=None, row_scale_group=0):
+         a_off=0, b_off=0, c_off=0, inner=None, row_scale=None, row_scale_group=0, a16=None, b16=None, c16=None):
     """a_off/b_off/c_off: element offsets into A/B/C (column slices of wider buffers).
     inner=(n, a_bstride_inner, b_bstride_inner, c_bstride_inner): a two-level batch of
-    batch = outer * n entries (mdemi_gemm_desc.batch_inner), e.g. (image, head)."""
+    batch = outer * n entries (mdemi_gemm_desc.batch_inner), e.g. (image, head).
+    a16 / b16 / c16 (precision "bf16" only): bf16 copies of A / B (the RNE bf16 of the fp32
+    tensors, same layout; A / B may then be None) and a bf16 copy of C to write -- the bf16
+    storage path (mdemi_gemm_bf16x), bit-identical to the fp32-operand bf16 GEMM."""
     if inner is not None and inner[0] > 1 and os.environ.get("MDEMI_GEMM_SPLIT_INNER") == "1":
         # debug/A-B path: the same products as one launch per inner index
         n, a2, b2, c2 = inner
@@ -134,8 +137,10 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     d.M, d.N, d.K, d.batch = M, N, K, batch
     if inner is not None and inner[0] > 1:
         d.batch_inner, d.a_bstride_inner, d.b_bstride_inner, d.c_bstride_inner = inner
-    d.A, d.lda, d.a_bstride, d.a_layout, d.a_op = A.data_ptr() + 4 * a_off, lda, a_bstride, a_layout, a_op
-    d.B, d.ldb, d.b_bstride, d.b_layout, d.b_op = B.data_ptr() + 4 * b_off, ldb, b_bstride, b_layout, b_op
+    d.A = A.data_ptr() + 4 * a_off if A is not None else None
+    d.B = B.data_ptr() + 4 * b_off if B is not None else None
+    d.lda, d.a_bstride, d.a_layout, d.a_op = lda, a_bstride, a_layout, a_op
+    d.ldb, d.b_bstride, d.b_layout, d.b_op = ldb, b_bstride, b_layout, b_op
     d.C, d.ldc, d.c_bstride = C.data_ptr() + 4 * c_off, ldc, c_bstride
     d.alpha, d.beta = alpha, beta
     d.bias, d.bias_mode, d.act = (bias.data_ptr() if bias is not None else None), bias_mode, act
@@ -155,7 +160,13 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     if need:
         ws = L.workspace(need, C.device, slot=1)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
-    if _PRECISION[0] == "bf16":
+    if a16 is not None or b16 is not None or c16 is not None:
+        if _PRECISION[0] != "bf16":
+            raise ValueError("gemm: bf16 operands / output (a16, b16, c16) need matmul precision 'bf16'")
+        L.check(lib.mdemi_gemm_bf16x(ctypes.byref(d), None if a16 is None else a16.data_ptr() + 2 * a_off,
+                                     None if b16 is None else b16.data_ptr() + 2 * b_off,
+                                     None if c16 is None else c16.data_ptr() + 2 * c_off, L.stream()), "gemm_bf16x")
+    elif _PRECISION[0] == "bf16":
         L.check(lib.mdemi_gemm_bf16(ctypes.byref(d), L.stream()), "gemm_bf16")
     elif _PRECISION[0] == "fp32e":
         L.check(lib.mdemi_gemm_f32e(ctypes.byref(d), L.stream()), "gemm_f32e")

@@ -236,8 +236,8 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
     instead (test_every_bf16_gemm_of_the_configs4_step_is_exact).
 
     Outputs (depth, centres, the 8 attention maps): max|gpu - o64| <= 20 x max|o32 - o64| +
-    1e-3 x max|o64|; depth and centres within BF16_OUT_L2 relative L2 of plain (what bf16
-    costs against the fp32 model).  depthformer_v8.py:46-75, decoder_v8.py:97-171,
+    1e-3 x max|o64|; depth and centres within twice the emulation's relative L2 distance from
+    plain (what bf16 costs against the fp32 model, printed for both).  depthformer_v8.py:46-75, decoder_v8.py:97-171,
     luna_layer.py:181-259."""
     import contextlib
 
@@ -309,9 +309,15 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
         return (torch.linalg.norm(a - ref) / torch.linalg.norm(ref)).item()
 
     cost = {k: rel_l2(g, ref) for k, g, ref in zip(names, gpu_out, plain)}
+    emu_cost = {k: rel_l2(r, ref) for k, r, ref in zip(names, o64, plain)}
     print(f"configs[4] bf16: worst max-error / magnitude vs the bf16-emulating fp64 oracle "
-          f"{sorted(worst, reverse=True)[:5]}; relative L2 vs the fp32-numerics fp64 oracle {cost}")
-    assert cost["depth"] <= BF16_OUT_L2 and cost["centers"] <= BF16_OUT_L2, cost
+          f"{sorted(worst, reverse=True)[:5]}; relative L2 vs the fp32-numerics fp64 oracle: GPU {cost}, "
+          f"bf16 emulation {emu_cost}")
+    # what bf16 costs against the fp32 model is the model's, not the kernels': the GPU's distance
+    # from the un-rounded model stays within twice the emulation's (peaked bin probabilities
+    # make the depth itself move ~1.5 % under bf16 here)
+    for k in ("depth", "centers"):
+        assert cost[k] <= 2.0 * emu_cost[k] + 1e-3, (k, cost[k], emu_cost[k])
 
 
 def test_every_bf16_gemm_of_the_configs4_step_is_exact(mf):

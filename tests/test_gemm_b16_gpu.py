@@ -1,0 +1,160 @@
+"""bf16-operand GEMM (csrc/gemm_b16_kernel.h, mdemi_gemm_bf16x): operands stored in bf16
+and DMA'd straight into LDS.  For operands that are the RNE bf16 of fp32 tensors, every
+result must be BIT-IDENTICAL to the bf16 GEMM on the fp32 tensors (mdemi_gemm_bf16, which
+rounds the same values as it stages them) -- on every layout pair the model uses (dense
+k-/m,n-contiguous, implicit-im2col forward / data gradient / weight gradient, zero and
+replicate padding), batched and two-level-batched products, split K and the tail split,
+ragged edges, every fused epilogue, both tile variants -- and the optional bf16 output copy
+must equal the RNE bf16 of the fp32 output.  Layouts the DMA loaders cannot stage fall back
+to the fp32-operand kernel.  Reference: the autocast bf16 conv / linear / bmm of
+model/Depthformer/layer_utils.py:6-34, luna_layer.py:181-259 (BASELINE configs[4])."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def mf():
+    from mdemi import _lib
+    from mdemi import functional
+    _lib.load()
+    return functional
+
+
+def _b(t):
+    return t.to(torch.bfloat16)
+
+
+def _run(mf, L, fp, bf, C_shape, variant, **kw):
+    """C from the fp32-operand bf16 GEMM and from the bf16-operand one (forced variant)."""
+    lib = L.load()
+    A, B = fp
+    A16, B16 = bf
+    ref = torch.full(C_shape, float("nan"), device=DEV)
+    got = torch.full(C_shape, float("nan"), device=DEV)
+    c16 = torch.empty(C_shape, device=DEV, dtype=torch.bfloat16)
+    with mf.matmul_precision("bf16"):
+        mf.gemm(A, B, ref, **kw)
+        assert lib.mdemi_gemm_set_variant_b16(variant) == 0
+        try:
+            mf.gemm(None, None, got, a16=A16, b16=B16, c16=c16, **kw)
+        finally:
+            lib.mdemi_gemm_set_variant_b16(-1)
+    torch.cuda.synchronize()
+    return ref, got, c16
+
+
+def _check(ref, got, c16, what):
+    assert torch.equal(ref, got), (what, (ref - got).abs().max().item())
+    assert torch.equal(c16, ref.to(torch.bfloat16)), what
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(3000, 384, 640), (1000, 200, 136), (4736, 1024, 256), (64, 96, 40000)])
+def test_dense_layouts_bit_identical(mf, variant, M, N, K):
+    from mdemi import _lib as L
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) * 0.05
+    bias = torch.randn(N, device=DEV)
+    dy = torch.randn(M, N, device=DEV)
+    res = torch.randn(M, N, device=DEV)
+    x, w, dy = (_b(t).float() for t in (x, w, dy))  # exactly representable: the bf16 copies are exact
+    # forward: Y = X W^T + b, SiLU, + residual  (KCONTIG x KCONTIG)
+    ref, got, c16 = _run(mf, L, (x, w), (_b(x), _b(w)), (M, N), variant, M=M, N=N, K=K, lda=K, ldb=K, ldc=N,
+                         a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG, bias=bias, bias_mode=L.BIAS_COL,
+                         act=L.ACT_SILU, residual=res, ldres=N, split_k=1)
+    _check(ref, got, c16, "fwd")
+    # data gradient: dX = dY W  (KCONTIG x MNCONTIG)
+    ref, got, c16 = _run(mf, L, (dy, w), (_b(dy), _b(w)), (M, K), variant, M=M, N=K, K=N, lda=N, ldb=K, ldc=K,
+                         a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
+    _check(ref, got, c16, "dgrad")
+    # weight gradient: dW = dY^T X  (MNCONTIG x MNCONTIG), split K over the M rows
+    ref, got, c16 = _run(mf, L, (dy, x), (_b(dy), _b(x)), (N, K), variant, M=N, N=K, K=M, lda=N, ldb=K, ldc=K,
+                         a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG, split_k=max(1, M // 512))
+    _check(ref, got, c16, "wgrad")
+    # m-contiguous A with k-contiguous B (MNCONTIG x KCONTIG): X^T-style product
+    ref, got, c16 = _run(mf, L, (x, dy), (_b(x), _b(dy)), (K, N), variant, M=K, N=N, K=M, lda=K, ldb=M, ldc=N,
+                         a_layout=L.L_MNCONTIG, b_layout=L.L_KCONTIG)
+    _check(ref, got, c16, "mn x kc")
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("cin,cout,k,pad,hw,mode", [(64, 96, 3, 1, (17, 23), "zero"), (128, 64, 3, 1, (30, 40), "rep"),
+                                                    (32, 40, 5, 2, (9, 12), "zero"), (256, 256, 3, 1, (60, 80), "zero")])
+def test_conv_layouts_bit_identical(mf, variant, cin, cout, k, pad, hw, mode):
+    from mdemi import _lib as L
+    torch.manual_seed(1)
+    n = 2
+    h, w = hw
+    pm = L.PAD_REPLICATE if mode == "rep" else L.PAD_ZERO
+    x = _b(torch.randn(n, h, w, cin, device=DEV)).float()
+    wt = _b(torch.randn(cout, k * k * cin, device=DEV) * 0.05).float()  # (ky,kx,c)-ordered rows
+    dy = _b(torch.randn(n, h, w, cout, device=DEV)).float()
+    M, K = n * h * w, k * k * cin
+    g = mf._geom(n, h, w, cin, h, w, k, k, 1, pad, pm)
+    ref, got, c16 = _run(mf, L, (x, wt), (_b(x), _b(wt)), (n, h, w, cout), variant, M=M, N=cout, K=K, lda=0, ldb=K,
+                         ldc=cout, a_layout=L.L_CONV, b_layout=L.L_KCONTIG, conv=g)
+    _check(ref, got, c16, "conv fwd")
+    # weight gradient: dW[co][(ky,kx,c)] = sum_pixels dY[p][co] x im2col(X)[p][(ky,kx,c)]
+    ref, got, c16 = _run(mf, L, (dy, x), (_b(dy), _b(x)), (cout, K), variant, M=cout, N=K, K=M, lda=cout, ldb=0,
+                         ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_CONV, conv=g, split_k=max(1, M // 1024))
+    _check(ref, got, c16, "conv wgrad")
+    if mode == "zero":  # data gradient: dX = conv(dY, flip(W)^T) with pad k-1-p (wd [(ky,kx,co)][c])
+        wd = _b(torch.randn(k * k * cout, cin, device=DEV) * 0.05).float()
+        gd = mf._geom(n, h, w, cout, h, w, k, k, 1, k - 1 - pad, L.PAD_ZERO)
+        ref, got, c16 = _run(mf, L, (dy, wd), (_b(dy), _b(wd)), (n, h, w, cin), variant, M=M, N=cin, K=k * k * cout,
+                             lda=0, ldb=cin, ldc=cin, a_layout=L.L_CONV, b_layout=L.L_MNCONTIG, conv=gd)
+        _check(ref, got, c16, "conv dgrad")
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_batched_attention_products_bit_identical(mf, variant):
+    """Two-level batch (image, head) as the Luna / self-attention products issue them:
+    scores = Q K^T (k-contiguous both), out = P V (V m/n-contiguous)."""
+    from mdemi import _lib as L
+    torch.manual_seed(2)
+    b, heads, S, T, d = 2, 4, 1200, 256, 64
+    q = _b(torch.randn(b, S, heads * d, device=DEV)).float()
+    kk = _b(torch.randn(b, T, heads * d, device=DEV)).float()
+    p = _b(torch.rand(b * heads, S, T, device=DEV)).float()
+    inner = (heads, d, d, S * T)
+    ref, got, c16 = _run(mf, L, (q, kk), (_b(q), _b(kk)), (b * heads, S, T), variant, M=S, N=T, K=d, lda=heads * d,
+                         ldb=heads * d, ldc=T, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG, batch=b * heads,
+                         a_bstride=S * heads * d, b_bstride=T * heads * d, c_bstride=heads * S * T, inner=inner)
+    _check(ref, got, c16, "scores")
+    inner2 = (heads, S * T, d, d)
+    ref, got, c16 = _run(mf, L, (p, kk), (_b(p), _b(kk)), (b, S, heads * d), variant, M=S, N=d, K=T, lda=T,
+                         ldb=heads * d, ldc=heads * d, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG, batch=b * heads,
+                         a_bstride=heads * S * T, b_bstride=T * heads * d, c_bstride=S * heads * d, inner=inner2)
+    _check(ref, got, c16, "p v")
+
+
+def test_unstageable_layout_falls_back(mf):
+    """K % 8 != 0 (a k-contiguous 16-B chunk would straddle the K edge): the fp32 operands are
+    used (same products), and without them the call refuses rather than guess."""
+    from mdemi import _lib as L
+    lib = L.load()
+    torch.manual_seed(3)
+    M, N, K = 300, 200, 100
+    x = _b(torch.randn(M, K, device=DEV)).float()
+    w = _b(torch.randn(N, K, device=DEV)).float()
+    d = L.GemmDesc()
+    d.M, d.N, d.K, d.batch, d.lda, d.ldb, d.ldc = M, N, K, 1, K, K, N
+    d.a_layout = d.b_layout = L.L_KCONTIG
+    d.split_k = 1
+    assert lib.mdemi_gemm_bf16x_supported(d, _b(x).data_ptr(), _b(w).data_ptr()) == 0
+    ref = torch.empty(M, N, device=DEV)
+    got = torch.empty(M, N, device=DEV)
+    c16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    with mf.matmul_precision("bf16"):
+        mf.gemm(x, w, ref, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG)
+        mf.gemm(x, w, got, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+                a16=_b(x), b16=_b(w), c16=c16)
+        with pytest.raises(RuntimeError, match="no bf16 path"):
+            mf.gemm(None, None, got, M, N, K, lda=K, ldb=K, ldc=N, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
+                    a16=_b(x), b16=_b(w))
+    torch.cuda.synchronize()
+    _check(ref, got, c16, "fallback")

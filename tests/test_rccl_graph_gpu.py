@@ -196,7 +196,7 @@ def test_newcrfs_large07_kitti_ddp_rccl_matches_single_process(rccl):
     ddp.model.load_state_dict(single.model.state_dict())
     assert single.ddp is None and ddp.ddp is not None
     grad_bytes = sum(ddp.ddp.bucket_bytes)
-    assert grad_bytes >= 1.08e9 and len(ddp.ddp.buckets) >= 16, (grad_bytes, len(ddp.ddp.buckets))
+    assert grad_bytes >= 1.08e9 and len(ddp.ddp.buckets) >= 14, (grad_bytes, len(ddp.ddp.buckets))
 
     def batch(seed):  # SURVEY §8d KITTI: U(1, 80) depth at a Bernoulli(0.15) LiDAR-like mask
         g = torch.Generator().manual_seed(seed)
