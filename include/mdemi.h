@@ -156,6 +156,9 @@ int mdemi_gemm_f32e(const mdemi_gemm_desc* d, void* stream);
  * Replaces the autocast bf16 conv/linear/bmm of model/Depthformer/layer_utils.py:6-34,
  * luna_layer.py:181-259, decoder_v8.py:97-171. */
 int mdemi_gemm_bf16x(const mdemi_gemm_desc* d, const void* a16, const void* b16, void* c16, void* stream);
+/* y[i] = RNE bf16 of x[i] (n elements; x, y 16-B aligned): the bf16 copy of an fp32 operand
+ * that no producer wrote in bf16 (precision "bf16" GEMM operands, mdemi_gemm_bf16x). */
+int mdemi_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 /* 1 when mdemi_gemm_bf16x would take the bf16-operand path for this descriptor. */
 int mdemi_gemm_bf16x_supported(const mdemi_gemm_desc* d, const void* a16, const void* b16);
 /* tuning hook of the bf16-operand family: 0 = 128-row tile, 1 = 256-row tile, -1 = per-shape

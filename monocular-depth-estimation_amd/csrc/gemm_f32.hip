@@ -56,20 +56,26 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const fl
     const int i = (int)(rem / p.N) + p.m_split, j = (int)(rem - (int64_t)(i - p.m_split) * p.N);
     const float* src = p.slab + (int64_t)b * MN + rem;
     float* dst = p.C + boff(p, b, p.c_bs, p.c_bs2) + (int64_t)i * p.ldc + j;
+    __bf16* dst16 = p.c16 ? reinterpret_cast<__bf16*>(p.c16) + (dst - p.C) : nullptr;  // C's layout
     if (quad) {
       float4 acc = *reinterpret_cast<const float4*>(src);
       for (int q = 1; q < p.split; ++q) {
         const float4 t = *reinterpret_cast<const float4*>(src + q * slab_stride);
         acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
       }
-      dst[0] = epilogue_value(p, b, i, j, acc.x);
-      dst[1] = epilogue_value(p, b, i, j + 1, acc.y);
-      dst[2] = epilogue_value(p, b, i, j + 2, acc.z);
-      dst[3] = epilogue_value(p, b, i, j + 3, acc.w);
+      const float v[4] = {epilogue_value(p, b, i, j, acc.x), epilogue_value(p, b, i, j + 1, acc.y),
+                          epilogue_value(p, b, i, j + 2, acc.z), epilogue_value(p, b, i, j + 3, acc.w)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dst[e] = v[e];
+        if (dst16) dst16[e] = (__bf16)v[e];
+      }
     } else {
       float acc = src[0];
       for (int q = 1; q < p.split; ++q) acc += src[q * slab_stride];
-      dst[0] = epilogue_value(p, b, i, j, acc);
+      const float v = epilogue_value(p, b, i, j, acc);
+      dst[0] = v;
+      if (dst16) dst16[0] = (__bf16)v;
     }
   }
   if (rs_part)
@@ -375,7 +381,7 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mod
   }
   const int64_t nblocks = (int64_t)p.tiles_m1 * p.tiles_n + (int64_t)p.tiles_m * p.tiles_n * d->batch * p.split;
   MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
-  const bool deep = p.split > 1 && colsum_combine(d, p);
+  const bool deep = p.split > 1 && colsum_combine(d, p) && !p.c16;  // the column-sum combine writes fp32 only
   if (p.split > 1 && !deep && (g_inline_reduce || p.m_split > 0)) {
     p.tile_cnt = tile_counters((int64_t)p.tiles_m * p.tiles_n * d->batch, st);
     if (p.tile_cnt && rowsum_part) p.rowsum_out = d->rowsum_a;  // the last arrivers sum the row partials

@@ -3,6 +3,8 @@
 // reference's run.py/optimizer construction is absent; config keys
 // optimizer.lr/weight_decay/betas/eps and train.grad_norm, e.g.
 // json/nyu/newcrfs/newcrfs_github_eval.json).
+#include <algorithm>
+
 #include "common.h"
 
 namespace mdemi {
@@ -266,6 +268,35 @@ extern "C" int mdemi_elementwise(int32_t op, const float* a, const float* b, flo
   nb = nb < 8192 ? nb : 8192;
   hipLaunchKernelGGL(ew_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, op, a, b, y, n, s, t);
   return check_launch("elementwise");
+}
+
+namespace mdemi {
+typedef __bf16 cast_bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float cast_f32x8_t __attribute__((ext_vector_type(8)));
+// y = RNE bf16 of x: 8 elements per thread (two 16-B loads, one 16-B store), grid-stride;
+// the tail (n % 8) by the first threads one element each
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ x, __bf16* __restrict__ y,
+                                                        int64_t n) {
+  const int64_t n8 = n / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const float4 a = reinterpret_cast<const float4*>(x)[2 * i], b = reinterpret_cast<const float4*>(x)[2 * i + 1];
+    const cast_f32x8_t v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    reinterpret_cast<cast_bf16x8_t*>(y)[i] = __builtin_convertvector(v, cast_bf16x8_t);
+  }
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n - 8 * n8) y[8 * n8 + t] = (__bf16)x[8 * n8 + t];
+}
+}  // namespace mdemi
+
+extern "C" int mdemi_cast_bf16(const float* x, void* y, int64_t n, void* stream) {
+  MDEMI_REQUIRE(x && y && n >= 0, "cast_bf16: bad args");
+  MDEMI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "cast_bf16: x and y must be 16-B aligned");
+  if (n == 0) return MDEMI_OK;
+  int64_t nb = cdiv(std::max<int64_t>(n / 8, 8), 256);
+  nb = nb < 16384 ? nb : 16384;
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, x, (__bf16*)y, n);
+  return check_launch("cast_bf16");
 }
 
 namespace mdemi {

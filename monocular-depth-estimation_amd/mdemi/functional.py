@@ -97,6 +97,60 @@ def get_matmul_precision() -> str:
     return _PRECISION[0]
 
 
+# bf16 storage of GEMM operands (precision "bf16"): every GEMM whose operands the DMA loaders
+# can stage reads bf16 copies (mdemi_gemm_bf16x) -- written by the producing kernel where it
+# can (set_b16), else by one cast sweep on first use, reused by every later GEMM on the same
+# tensor (the forward product and the weight gradient read the same activation).  The copies
+# are the RNE bf16 the fp32-operand bf16 GEMM rounds to as it stages, so results are
+# bit-identical; only bias-gradient row sums move from the GEMM to a column-sum sweep over the
+# same fp32 values.  MDEMI_BF16_STORAGE=0 (or set_bf16_storage(False)) keeps every operand fp32.
+_B16_STORAGE = [os.environ.get("MDEMI_BF16_STORAGE", "1") != "0"]
+
+
+def set_bf16_storage(on: bool) -> None:
+    _B16_STORAGE[0] = bool(on)
+
+
+def get_bf16_storage() -> bool:
+    return _B16_STORAGE[0]
+
+
+def set_b16(t, b16):
+    """Record b16 (a bf16 tensor, t's shape, contiguous) as the RNE bf16 copy of t; valid
+    while t is not modified in place (t._version)."""
+    t._mdemi_b16 = (b16, t._version)
+    return t
+
+
+def b16_of(t, convert=True):
+    """The bf16 copy of contiguous fp32 tensor t: the recorded one (set_b16) if still valid,
+    else (convert) a cast sweep, recorded on t unless t is a parameter (updated in place by the
+    optimizer through raw pointers, which torch's version counter does not see).  None for a
+    tensor that cannot be copied this way (non-contiguous, unaligned)."""
+    rec = t.__dict__.get("_mdemi_b16")
+    if rec is not None and rec[1] == t._version and rec[0].numel() == t.numel():
+        return rec[0]
+    base = t._base
+    if base is not None and base.data_ptr() == t.data_ptr() and base.numel() == t.numel():
+        rec = base.__dict__.get("_mdemi_b16")
+        if rec is not None and rec[1] == base._version and rec[0].numel() == t.numel():
+            return rec[0]
+    if not convert or not t.is_contiguous() or t.data_ptr() % 16 or t.dtype != torch.float32:
+        return None
+    b = torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
+    L.call("mdemi_cast_bf16", t.data_ptr(), b.data_ptr(), t.numel(), L.stream())
+    if not (t.is_leaf and t.requires_grad):
+        set_b16(t, b)
+    return b
+
+
+def new_b16_like(t):
+    """A bf16 buffer for a producer to write t's copy into (bf16 storage on), else None."""
+    if _PRECISION[0] != "bf16" or not _B16_STORAGE[0]:
+        return None
+    return torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
+
+
 class matmul_precision:
     """Context manager: with matmul_precision("bf16"): ..."""
 
@@ -160,6 +214,20 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     if need:
         ws = L.workspace(need, C.device, slot=1)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+    if (_PRECISION[0] == "bf16" and _B16_STORAGE[0] and a16 is None and b16 is None and a_op == L.OP_NONE
+            and b_op == L.OP_NONE and A is not None and B is not None):
+        a16, b16 = _b16_operands(d, A, B, a_off, b_off, rowsum_a, lib)
+        if a16 is not None and rowsum_a is not None:
+            # the bias-gradient row sums of the unrounded fp32 A: a column sum over A's k rows
+            # (A m-contiguous [K][M]), instead of the GEMM's in-kernel sums
+            ws = L.workspace(lib.mdemi_colsum_workspace_size(K, M), C.device, slot=2)
+            L.check(lib.mdemi_colsum_f32(A.data_ptr() + 4 * a_off, K, M, lda, rowsum_a.data_ptr(), 0, ws.data_ptr(),
+                                         L.stream()), "colsum")
+            d.rowsum_a = None
+            need = lib.mdemi_gemm_workspace_size(ctypes.byref(d))
+            if need:
+                ws = L.workspace(need, C.device, slot=1)
+                d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     if a16 is not None or b16 is not None or c16 is not None:
         if _PRECISION[0] != "bf16":
             raise ValueError("gemm: bf16 operands / output (a16, b16, c16) need matmul precision 'bf16'")
@@ -173,6 +241,26 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     else:
         L.check(lib.mdemi_gemm_f32(ctypes.byref(d), L.stream()), "gemm_f32")
     return C
+
+
+def _b16_operands(d, A, B, a_off, b_off, rowsum_a, lib):
+    """(a16, b16) for a bf16 GEMM the bf16-operand kernel can run (bf16 storage on), else
+    (None, None).  The layout check runs on the fp32 descriptor before any copy is made."""
+    for t in (A, B):
+        if not t.is_contiguous() or t.data_ptr() % 16:
+            return None, None
+    if a_off % 8 or b_off % 8:  # the bf16 slices must start 16-B aligned
+        return None, None
+    rs = d.rowsum_a
+    d.rowsum_a = None  # the row sums are taken by a column sum instead (gemm)
+    ok = lib.mdemi_gemm_bf16x_supported(ctypes.byref(d), A.data_ptr(), B.data_ptr())
+    d.rowsum_a = rs
+    if not ok:
+        return None, None
+    a16, b16 = b16_of(A), b16_of(B)
+    if a16 is None or b16 is None:
+        return None, None
+    return a16, b16
 
 
 def colsum(x2d, out=None, accumulate=False):

@@ -158,3 +158,67 @@ def test_unstageable_layout_falls_back(mf):
                     a16=_b(x), b16=_b(w))
     torch.cuda.synchronize()
     _check(ref, got, c16, "fallback")
+
+
+@pytest.mark.parametrize("bn", ["train", "eval"])
+def test_bf16_storage_step_matches_fp32_operand_step(mf, bn):
+    """The bf16 storage path (every bf16 GEMM on bf16 copies: producer-written or one cast per
+    tensor, reused by the later GEMMs on it) against the same Depthformer v8 forward + backward
+    with every operand fp32 (set_bf16_storage(False)): outputs, attention maps and every
+    gradient bit-identical, except the conv / linear bias gradients, which the storage path sums
+    from the same unrounded fp32 dY in a column-sum sweep instead of inside the GEMM (fp32
+    reassociation only)."""
+    from mdemi.model.Depthformer import DepthformerV8
+    from oracle.weights import closed_form_fill, rng_array
+    opt = {"hidden_dim": 64, "num_heads": 4, "num_bins": 64, "num_aux": 32, "img_size": [128, 160],
+           "attn_drop_prob": 0.0, "drop_prob": 0.0}
+    torch.manual_seed(0)
+    m = DepthformerV8.build(opt, 1e-3, 10.0)
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    closed_form_fill(sd, seed=0.61, scale=0.03)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    if bn == "eval":
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.eval()
+    img = torch.from_numpy(rng_array((2, 3, 128, 160), 31)).float().to(DEV)
+    dy = torch.from_numpy(rng_array((2, 1, 64, 80), 32)).float().to(DEV)
+
+    def run(storage):
+        prev = mf.get_bf16_storage()
+        mf.set_bf16_storage(storage)
+        m.load_state_dict({k: v.to(DEV) for k, v in sd.items()})
+        m.zero_grad(set_to_none=True)
+        try:
+            with mf.matmul_precision("bf16"):
+                depth, centers, attn = m(img)
+                (depth * dy).sum().backward()
+        finally:
+            mf.set_bf16_storage(prev)
+        torch.cuda.synchronize()
+        return [depth.detach().clone(), centers.detach().clone()] + [a.detach().clone() for a in attn], \
+            {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+
+    out0, g0 = run(False)
+    out1, g1 = run(True)
+    for i, (a, b) in enumerate(zip(out0, out1)):
+        assert torch.equal(a, b), i
+    n_bias, worst = 0, (0.0, None)
+    for k in g0:
+        if k.endswith(".bias") and not torch.equal(g0[k], g1[k]):
+            n_bias += 1
+            import bf16_criterion as crit
+            sh = crit.SHIFT_INVARIANT.search(k)
+            if sh:  # exact gradient zero (softmax shift invariance): both are residue, held in size
+                vb = k[:sh.start()] + crit._VALUE_OF[sh.group(1)] + ".bias"
+                lim = 1e-4 * g0[vb].abs().max().item()
+                assert g0[k].abs().max().item() <= lim and g1[k].abs().max().item() <= lim, k
+            else:  # fp32 reassociation of a sum over every pixel: relative L2 within 1e-4
+                rel = ((g1[k] - g0[k]).norm() / g0[k].norm().clamp_min(1e-30)).item()
+                worst = max(worst, (rel, k))
+                assert rel <= 1e-4, (k, rel)
+        else:
+            assert torch.equal(g0[k], g1[k]), k
+    print(f"bf16 storage step == fp32-operand bf16 step bit for bit; {n_bias} bias gradients reassociated "
+          f"(worst relative L2 {worst})")
