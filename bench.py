@@ -296,19 +296,22 @@ def measure_files(args, trainer, pipe, B, world):
 
 
 # --------------------------------------------------------------------------- roofline
-def _gemm_alg_bytes(A, B, M, N, K, kw):
-    """Algorithmic HBM bytes of one GEMM launch: every operand read once, C written once
-    (conv operands: the NHWC activation, not its im2col)."""
+def _gemm_alg_bytes(A, B, M, N, K, kw, ob=4.0):
+    """Algorithmic HBM bytes of one GEMM launch: every operand read once (ob bytes per element:
+    4 fp32, 2 on the bf16-operand path), C written once in fp32 (plus its bf16 copy when one is
+    requested); conv operands count the NHWC activation, not its im2col."""
     def operand(layout, rows, cols):
         if layout == 2:  # implicit im2col: the activation tensor
             g = kw["conv"]
-            return 4.0 * g.n * g.h * g.w * g.c
-        return 4.0 * rows * cols
+            return ob * g.n * g.h * g.w * g.c
+        return ob * rows * cols
     batch = kw.get("batch", 1)
     b = operand(kw.get("a_layout"), M, K) + operand(kw.get("b_layout"), K, N)
     b *= batch if kw.get("a_layout") != 2 else 1
     c = 4.0 * M * N * batch
     b += c * (2 if kw.get("beta", 0.0) else 1)
+    if kw.get("c16") is not None:
+        b += c / 2
     for extra in ("aux", "residual", "preact"):
         if kw.get(extra) is not None:
             b += c
@@ -388,8 +391,10 @@ def gemm_roofline(trainer, batches):
         s.record(torch.cuda.current_stream())
         out = orig(A, B, C, M, N, K, **kw)
         e.record(torch.cuda.current_stream())
-        key = (kw.get("a_layout"), kw.get("b_layout"), kw.get("a_op", 0), kw.get("b_op", 0))
-        recs.append((key, 2.0 * M * N * K * kw.get("batch", 1), _gemm_alg_bytes(A, B, M, N, K, kw), s, e))
+        path = mf.LAST_GEMM[0]  # "b16": bf16 operands in HBM (gemm_b16_kernel)
+        key = (path, kw.get("a_layout"), kw.get("b_layout"), kw.get("a_op", 0), kw.get("b_op", 0))
+        recs.append((key, 2.0 * M * N * K * kw.get("batch", 1),
+                     _gemm_alg_bytes(A, B, M, N, K, kw, ob=2.0 if path == "b16" else 4.0), s, e))
         return out
 
     mf.gemm = timed
@@ -427,31 +432,49 @@ def profiled_traffic(regex, workload):
     return None if fam is None else fam.get("traffic_bytes_per_launch")
 
 
+def _family(key, prec):
+    """(kernel name, MFMA peak TF/s, rocprofv3 regex) of a GEMM family key (path, al, bl, aop, bop)."""
+    path, al, bl, aop, bop = key
+    if path == "b16":  # bf16 operands in HBM, direct-to-LDS (gemm_b16_kernel.h)
+        return "gemm_b16_kernel", BF16_MFMA_PEAK_TFLOPS, f"gemm_b16_kernel<{al}, {bl},"
+    if prec == "fp32":  # register-staged gemm_f32_kernel and direct-to-LDS gemm_glds_kernel: one family
+        return "gemm_f32_kernel|gemm_glds_kernel", FP32_MFMA_PEAK_TFLOPS, f"gemm_f32<{al}, {bl}, {aop}, {bop}>"
+    np_ = 1 if prec == "bf16" else 3  # the 16-bit family: NP = 1 (bf16) or 3 (fp32e) planes
+    return ("gemm_m16_kernel", BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else F32E_MFMA_PEAK_TFLOPS,
+            f"gemm_m16_kernel<{al}, {bl}, {aop}, {bop}, {np_},")
+
+
+def _bound(fl, t, alg, peak):
+    """The roofline that bounds a family: MFMA when its algorithmic intensity (FLOP per HBM
+    byte) exceeds the machine balance peak / 8 TB/s, else HBM."""
+    if fl / max(alg, 1.0) >= peak * 1e12 / (HBM_PEAK_GBS * 1e9):
+        return "mfma", fl / t / 1e12, peak, "TFLOP/s"
+    return "hbm", alg / t / 1e9, HBM_PEAK_GBS, "GB/s"
+
+
 def roofline_entry(trainer, batches, workload_key, ms):
     by, dom, tot_fl, tot_t = gemm_roofline(trainer, batches)
-    (al, bl, aop, bop), (fl, t, cnt, alg) = dom
-    ach = fl / t / 1e12
+    key, (fl, t, cnt, alg) = dom
+    _, al, bl, aop, bop = key
     prec = trainer.precision
-    if prec == "fp32":  # register-staged gemm_f32_kernel and direct-to-LDS gemm_glds_kernel: one family
-        kname, peak, regex = "gemm_f32_kernel|gemm_glds_kernel", FP32_MFMA_PEAK_TFLOPS, f"gemm_f32<{al}, {bl}, {aop}, {bop}>"
-    else:  # the 16-bit family: NP = 1 (bf16) or 3 (fp32e) planes
-        np_ = 1 if prec == "bf16" else 3
-        kname = "gemm_m16_kernel"
-        peak = BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else F32E_MFMA_PEAK_TFLOPS
-        regex = f"gemm_m16_kernel<{al}, {bl}, {aop}, {bop}, {np_},"
+    kname, peak, regex = _family(key, prec)
+    bound, ach, roof_peak, unit = _bound(fl, t, alg, peak)
     traffic = profiled_traffic(regex, workload_key)
     alg_pl = alg / cnt
-    roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4),
+    roof = {"bound": bound, "achieved": round(ach, 2), "peak": roof_peak, "unit": unit,
+            "frac": round(ach / roof_peak, 4),
             "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
             "algorithmic_bytes": round(alg_pl), "traffic_over_algorithmic":
                 (round(traffic / alg_pl, 3) if traffic else None),
             "kernel": f"{kname}<{KERNEL_NAME[al]},{KERNEL_NAME[bl]},{aop},{bop}> ({prec}; all pipelining variants)",
             "kernel_regex": regex, "launches": cnt, "avg_launch_us": round(t / cnt * 1e6, 2),
-            "flops_per_launch": fl / cnt}
-    fams = {f"{KERNEL_NAME[k[0]]},{KERNEL_NAME[k[1]]},{k[2]},{k[3]}": {
-        "launches": v[2], "ms_per_step": round(v[1] * 1e3, 3), "tflops": round(v[0] / v[1] / 1e12, 2),
-        "algorithmic_GBps": round(v[3] / v[1] / 1e9, 1)} for k, v in sorted(by.items(), key=lambda kv: -kv[1][1])}
+            "flops_per_launch": fl / cnt, "tflops": round(fl / t / 1e12, 2)}
+    fams = {}
+    for k, v in sorted(by.items(), key=lambda kv: -kv[1][1]):
+        b, a, pk, u = _bound(v[0], v[1], v[3], _family(k, prec)[1])
+        fams[f"{k[0]}:{KERNEL_NAME[k[1]]},{KERNEL_NAME[k[2]]},{k[3]},{k[4]}"] = {
+            "launches": v[2], "ms_per_step": round(v[1] * 1e3, 3), "tflops": round(v[0] / v[1] / 1e12, 2),
+            "algorithmic_GBps": round(v[3] / v[1] / 1e9, 1), "bound": b, "frac": round(a / pk, 4)}
     extra = {"gemm_all": {"achieved_tflops": round(tot_fl / tot_t / 1e12, 2), "gemm_ms_per_step": round(tot_t * 1e3, 2),
                           "gemm_tflop_per_step": round(tot_fl / 1e12, 3),
                           "frac": round(tot_fl / tot_t / 1e12 / peak, 4), "families": fams},

@@ -159,6 +159,9 @@ int mdemi_gemm_bf16x(const mdemi_gemm_desc* d, const void* a16, const void* b16,
 /* y[i] = RNE bf16 of x[i] (n elements; x, y 16-B aligned): the bf16 copy of an fp32 operand
  * that no producer wrote in bf16 (precision "bf16" GEMM operands, mdemi_gemm_bf16x). */
 int mdemi_cast_bf16(const float* x, void* y, int64_t n, void* stream);
+/* y = a + b with its RNE bf16 copy y16 (n % 4 == 0): a residual sum that the next bf16 GEMM
+ * reads as its operand (the bf16 storage path). */
+int mdemi_add16(const float* a, const float* b, float* y, void* y16, int64_t n, void* stream);
 /* 1 when mdemi_gemm_bf16x would take the bf16-operand path for this descriptor. */
 int mdemi_gemm_bf16x_supported(const mdemi_gemm_desc* d, const void* a16, const void* b16);
 /* tuning hook of the bf16-operand family: 0 = 128-row tile, 1 = 256-row tile, -1 = per-shape
@@ -363,6 +366,18 @@ int mdemi_bn_train_fwd(const float* x, const float* gamma, const float* beta, fl
                        float* rstd, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                        float momentum, int32_t N, int64_t HW, int32_t C, float eps, int32_t act,
                        void* workspace, void* stream);
+/* the same, also writing y16 (may be NULL): the RNE bf16 copy of y that a following bf16 GEMM
+ * reads (the bf16 storage path of precision "bf16", layer_utils.py:6-34 ConvBN -> conv). */
+int mdemi_bn_train_fwd16(const float* x, const float* gamma, const float* beta, float* y, void* y16,
+                         float* mean, float* rstd, float* running_mean, float* running_var,
+                         int64_t* num_batches_tracked, float momentum, int32_t N, int64_t HW, int32_t C,
+                         float eps, int32_t act, void* workspace, void* stream);
+/* mdemi_chnorm_bwd (BatchNorm) also writing dx16 (may be NULL): the RNE bf16 copy of dx, the
+ * output gradient of the conv before the BN that its data- and weight-gradient GEMMs read. */
+int mdemi_chnorm_bwd16(const float* dy, const float* x, const float* y, const float* mean,
+                       const float* rstd, const float* gamma, const float* beta, float* dx, void* dx16,
+                       float* dgamma, float* dbeta, int32_t N, int64_t HW, int32_t C,
+                       int32_t groups, int32_t is_bn, int32_t act, void* workspace, void* stream);
 /* backward of mdemi_chnorm_apply for BatchNorm (eval-mode BN inside a training step:
  * frozen statistics, so dx = gamma * rstd * act'(pre) * dy with no batch terms);
  * dx may be NULL (input needs no gradient); dgamma and dbeta are both NULL (frozen

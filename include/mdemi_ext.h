@@ -50,6 +50,10 @@ int mdemi_spatial_reduce(const float* a, const float* b, float* out, int32_t N, 
                          float scale, void* workspace, void* stream);
 int mdemi_chan_scale(const float* x, const float* g, const float* add, float* y, int32_t N, int64_t HW,
                      int32_t C, void* stream);
+/* the same with y16 (may be NULL): the RNE bf16 copy of y (SqueezeExcite's output, read by
+ * the MBConv projection conv as a bf16 GEMM operand under precision "bf16") */
+int mdemi_chan_scale16(const float* x, const float* g, const float* add, float* y, void* y16, int32_t N,
+                       int64_t HW, int32_t C, void* stream);
 
 /* SqueezeExcite gate MLP (conv_reduce 1x1 + bias, swish, conv_expand 1x1 +  */
 /* bias, sigmoid) on pooled [N][C]; wr [R][C], we [C][R].  hid receives the  */

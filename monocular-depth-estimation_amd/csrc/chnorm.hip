@@ -66,7 +66,8 @@ __global__ __launch_bounds__(CN_THREADS) void gn_stats(const float* __restrict__
 __global__ __launch_bounds__(CN_THREADS) void chnorm_apply(const float* __restrict__ x, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, float* __restrict__ y,
-                                                           int N, int64_t HW, int C, int G, int is_bn, int act) {
+                                                           int N, int64_t HW, int C, int G, int is_bn, int act,
+                                                           __bf16* __restrict__ y16 = nullptr) {
   const int64_t total = (int64_t)N * HW * C;
   const int cpg = C / G;
   for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total; e += (int64_t)gridDim.x * CN_THREADS) {
@@ -74,6 +75,7 @@ __global__ __launch_bounds__(CN_THREADS) void chnorm_apply(const float* __restri
     const int s = is_bn ? c : (int)(e / (HW * C)) * G + c / cpg;
     const float v = (x[e] - mean[s]) * rstd[s] * gamma[c] + beta[c];
     y[e] = apply_act(act, v);
+    if (y16) y16[e] = (__bf16)y[e];
   }
 }
 
@@ -124,7 +126,8 @@ __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply(const float* __restri
                                                            const float* __restrict__ beta,
                                                            const float* __restrict__ dgamma,
                                                            const float* __restrict__ dbeta, float* __restrict__ dx,
-                                                           int64_t rows, int C, int act) {
+                                                           int64_t rows, int C, int act,
+                                                           __bf16* __restrict__ dx16 = nullptr) {
   const int64_t total = rows * C;
   const float inv_n = 1.f / (float)rows;
   for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total; e += (int64_t)gridDim.x * CN_THREADS) {
@@ -133,7 +136,9 @@ __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply(const float* __restri
     const float xh = (x[e] - mean[c]) * rs;
     const float pre = xh * ga + beta[c];
     const float d = dy[e] * act_grad(act, pre, apply_act(act, pre));
-    dx[e] = ga * rs * (d - inv_n * dbeta[c] - xh * inv_n * dgamma[c]);
+    const float o = ga * rs * (d - inv_n * dbeta[c] - xh * inv_n * dgamma[c]);
+    dx[e] = o;
+    if (dx16) dx16[e] = (__bf16)o;
   }
 }
 
@@ -199,6 +204,13 @@ __global__ __launch_bounds__(CN_THREADS) void gn_bwd_kernel(const float* __restr
 // block).  Elementwise passes are float4 with 32-bit quad indices.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float4 f4(float v) { return make_float4(v, v, v, v); }
+typedef __bf16 cn_bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float cn_f32x4_t __attribute__((ext_vector_type(4)));
+// the RNE bf16 copy of 4 consecutive outputs (8 B): the operand a later bf16 GEMM reads
+__device__ __forceinline__ void store_bf16x4(__bf16* p, float4 o) {
+  const cn_f32x4_t v = {o.x, o.y, o.z, o.w};
+  *reinterpret_cast<cn_bf16x4_t*>(p) = __builtin_convertvector(v, cn_bf16x4_t);
+}
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // PASS 0: sum x; PASS 1: sum (x - mean)^2; PASS 2 (backward): (sum d*xhat, sum d) with
@@ -348,7 +360,8 @@ template <int ACT = -1>
 __global__ __launch_bounds__(CN_THREADS) void bn_apply4(const float* __restrict__ x, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, float* __restrict__ y,
-                                                        int64_t total4, int CQ, int act) {
+                                                        int64_t total4, int CQ, int act,
+                                                        __bf16* __restrict__ y16 = nullptr) {
   if (ACT >= 0) act = ACT;
   for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
     const int c = 4 * (int)(e % CQ);
@@ -360,6 +373,7 @@ __global__ __launch_bounds__(CN_THREADS) void bn_apply4(const float* __restrict_
     o.z = apply_act(act, (v.z - mu.z) * rs.z * ga.z + be.z);
     o.w = apply_act(act, (v.w - mu.w) * rs.w * ga.w + be.w);
     reinterpret_cast<float4*>(y)[e] = o;
+    if (y16) store_bf16x4(y16 + 4 * e, o);
   }
 }
 
@@ -371,7 +385,8 @@ __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply4(const float* __restr
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ dgamma,
                                                             const float* __restrict__ dbeta, float* __restrict__ dx,
-                                                            int64_t total4, int CQ, float inv_n, int act) {
+                                                            int64_t total4, int CQ, float inv_n, int act,
+                                                            __bf16* __restrict__ dx16 = nullptr) {
   if (ACT >= 0) act = ACT;
   for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
     const int c = 4 * (int)(e % CQ);
@@ -389,6 +404,7 @@ __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply4(const float* __restr
     MDEMI_BNA(x) MDEMI_BNA(y) MDEMI_BNA(z) MDEMI_BNA(w)
 #undef MDEMI_BNA
     reinterpret_cast<float4*>(dx)[e] = o;
+    if (dx16) store_bf16x4(dx16 + 4 * e, o);
   }
 }
 
@@ -451,7 +467,7 @@ static float bn_unbias(int64_t rows) { return (float)((double)rows / (double)(ro
 
 static int chnorm_fwd_impl(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
                            int32_t N, int64_t HW, int32_t C, int32_t groups, int32_t is_bn, float eps, int32_t act,
-                           void* workspace, void* stream, BnRunning run) {
+                           void* workspace, void* stream, BnRunning run, __bf16* y16 = nullptr) {
   MDEMI_REQUIRE(x && gamma && beta && y && mean && rstd && N > 0 && HW > 0 && C > 0, "chnorm_fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   if (is_bn) {
@@ -474,7 +490,7 @@ static int chnorm_fwd_impl(const float* x, const float* gamma, const float* beta
                          (const float*)mean);
       const int64_t total4 = rows * C / 4;
       MDEMI_BN_ACT_LAUNCH(MDEMI_KT_APPLY4, act, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, x, gamma, beta, mean,
-                          rstd, y, total4, C / 4, act);
+                          rstd, y, total4, C / 4, act, y16);
       return check_launch("chnorm_fwd");
     }
     const int rpb = rows_per_block(rows);
@@ -484,7 +500,7 @@ static int chnorm_fwd_impl(const float* x, const float* gamma, const float* beta
     hipLaunchKernelGGL(bn_partial, dim3(nblk), dim3(CN_THREADS), 0, st, x, mean, part, rows, C, 1, rpb);
     hipLaunchKernelGGL(bn_combine, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, rows, 1, eps, mean, rstd);
     hipLaunchKernelGGL(chnorm_apply, dim3(grid_for(rows * C)), dim3(CN_THREADS), 0, st, x, gamma, beta, mean, rstd, y,
-                       N, HW, C, C, 1, act);
+                       N, HW, C, C, 1, act, y16);
     if (run.rmean)
       hipLaunchKernelGGL(bn_running_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, mean, rstd, run.rmean,
                          run.rvar, run.tracked, C, run.unbias, eps, run.m);
@@ -508,10 +524,20 @@ extern "C" int mdemi_bn_train_fwd(const float* x, const float* gamma, const floa
                                   float* rstd, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                                   float momentum, int32_t N, int64_t HW, int32_t C, float eps, int32_t act,
                                   void* workspace, void* stream) {
+  return mdemi_bn_train_fwd16(x, gamma, beta, y, nullptr, mean, rstd, running_mean, running_var, num_batches_tracked,
+                              momentum, N, HW, C, eps, act, workspace, stream);
+}
+
+extern "C" int mdemi_bn_train_fwd16(const float* x, const float* gamma, const float* beta, float* y, void* y16,
+                                    float* mean, float* rstd, float* running_mean, float* running_var,
+                                    int64_t* num_batches_tracked, float momentum, int32_t N, int64_t HW, int32_t C,
+                                    float eps, int32_t act, void* workspace, void* stream) {
   MDEMI_REQUIRE(running_mean && running_var, "bn_train_fwd: running statistics required");
+  MDEMI_REQUIRE(!y16 || ((uintptr_t)y16 & 7) == 0, "bn_train_fwd16: y16 must be 8-B aligned");
   const int64_t rows = (int64_t)N * HW;
   return chnorm_fwd_impl(x, gamma, beta, y, mean, rstd, N, HW, C, C, 1, eps, act, workspace, stream,
-                         BnRunning{running_mean, running_var, num_batches_tracked, bn_unbias(rows), momentum});
+                         BnRunning{running_mean, running_var, num_batches_tracked, bn_unbias(rows), momentum},
+                         (__bf16*)y16);
 }
 
 __global__ void gn_param_reduce(const float* __restrict__ part, int N, int C, float* dgamma, float* dbeta) {
@@ -530,7 +556,17 @@ extern "C" int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y,
                                 const float* gamma, const float* beta, float* dx, float* dgamma, float* dbeta,
                                 int32_t N, int64_t HW, int32_t C, int32_t groups, int32_t is_bn, int32_t act,
                                 void* workspace, void* stream) {
+  return mdemi_chnorm_bwd16(dy, x, y, mean, rstd, gamma, beta, dx, nullptr, dgamma, dbeta, N, HW, C, groups, is_bn, act,
+                            workspace, stream);
+}
+
+extern "C" int mdemi_chnorm_bwd16(const float* dy, const float* x, const float* y, const float* mean,
+                                  const float* rstd, const float* gamma, const float* beta, float* dx, void* dx16v,
+                                  float* dgamma, float* dbeta, int32_t N, int64_t HW, int32_t C, int32_t groups,
+                                  int32_t is_bn, int32_t act, void* workspace, void* stream) {
   (void)y;
+  __bf16* dx16 = (__bf16*)dx16v;
+  MDEMI_REQUIRE(!dx16 || (is_bn && ((uintptr_t)dx16 & 7) == 0), "chnorm_bwd16: dx16 needs BatchNorm and 8-B alignment");
   MDEMI_REQUIRE(dy && x && mean && rstd && gamma && beta && dx && dgamma && dbeta && N > 0 && HW > 0 && C > 0,
                 "chnorm_bwd: bad args");
   if (!workspace) { set_error("chnorm_bwd: workspace required"); return MDEMI_EWORKSPACE; }
@@ -547,7 +583,7 @@ extern "C" int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y,
                          dbeta);
       const int64_t total4 = rows * C / 4;
       MDEMI_BN_ACT_LAUNCH(MDEMI_KT_BWDAPPLY4, act, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd,
-                          gamma, beta, dgamma, dbeta, dx, total4, C / 4, 1.f / (float)rows, act);
+                          gamma, beta, dgamma, dbeta, dx, total4, C / 4, 1.f / (float)rows, act, dx16);
       return check_launch("chnorm_bwd");
     }
     const int rpb = rows_per_block(rows);
@@ -556,7 +592,7 @@ extern "C" int mdemi_chnorm_bwd(const float* dy, const float* x, const float* y,
                        C, act, rpb);
     hipLaunchKernelGGL(bn_bwd_combine, dim3((C + 255) / 256), dim3(256), 0, st, part, nblk, C, dgamma, dbeta);
     hipLaunchKernelGGL(bn_bwd_apply, dim3(grid_for(rows * C)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma, beta,
-                       dgamma, dbeta, dx, rows, C, act);
+                       dgamma, dbeta, dx, rows, C, act, dx16);
   } else {
     MDEMI_REQUIRE(groups > 0 && C % groups == 0, "chnorm_bwd: C %% groups != 0");
     hipLaunchKernelGGL(gn_bwd_kernel, dim3(N * groups), dim3(CN_THREADS), 0, st, dy, x, mean, rstd, gamma, beta, dx,

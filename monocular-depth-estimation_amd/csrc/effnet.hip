@@ -407,7 +407,8 @@ static int spatial_chunks(int N, int64_t HW, int C) {
 
 __global__ __launch_bounds__(256) void chan_scale_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                          const float* __restrict__ add, float* __restrict__ y,
-                                                         int64_t HW, int C, int64_t total4) {
+                                                         int64_t HW, int C, int64_t total4,
+                                                         __bf16* __restrict__ y16 = nullptr) {
   const int C4 = C >> 2;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total4; e += (int64_t)gridDim.x * 256) {
     const int c4 = (int)(e % C4);
@@ -420,6 +421,12 @@ __global__ __launch_bounds__(256) void chan_scale_kernel(const float* __restrict
       o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
     }
     reinterpret_cast<float4*>(y)[e] = o;
+    if (y16) {  // the RNE bf16 copy a following bf16 GEMM (conv_pwl) reads
+      typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v ov = {o.x, o.y, o.z, o.w};
+      reinterpret_cast<b4*>(y16)[e] = __builtin_convertvector(ov, b4);
+    }
   }
 }
 
@@ -648,10 +655,16 @@ extern "C" int mdemi_spatial_reduce(const float* a, const float* b, float* out, 
 
 extern "C" int mdemi_chan_scale(const float* x, const float* g, const float* add, float* y, int32_t N, int64_t HW,
                                 int32_t C, void* stream) {
+  return mdemi_chan_scale16(x, g, add, y, nullptr, N, HW, C, stream);
+}
+
+extern "C" int mdemi_chan_scale16(const float* x, const float* g, const float* add, float* y, void* y16, int32_t N,
+                                  int64_t HW, int32_t C, void* stream) {
   MDEMI_REQUIRE(x && g && y && N > 0 && HW > 0 && C > 0 && C % 4 == 0, "chan_scale: bad args (C %% 4 == 0)");
+  MDEMI_REQUIRE(!y16 || ((uintptr_t)y16 & 7) == 0, "chan_scale16: y16 must be 8-B aligned");
   const int64_t total4 = (int64_t)N * HW * C / 4;
   hipLaunchKernelGGL(chan_scale_kernel, dim3(grid_1d(total4)), dim3(256), 0, (hipStream_t)stream, x, g, add, y, HW, C,
-                     total4);
+                     total4, (__bf16*)y16);
   return check_launch("chan_scale");
 }
 

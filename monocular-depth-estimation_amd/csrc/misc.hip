@@ -287,7 +287,33 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n - 8 * n8) y[8 * n8 + t] = (__bf16)x[8 * n8 + t];
 }
+
+// y = a + b and its RNE bf16 copy y16, 4 elements per thread (n % 4 == 0, 16-B aligned)
+__global__ __launch_bounds__(256) void add16_kernel(const float4* __restrict__ a, const float4* __restrict__ b,
+                                                    float4* __restrict__ y, __bf16* __restrict__ y16, int64_t n4) {
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 u = a[i], v = b[i];
+    const float4 o = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+    y[i] = o;
+    const f4v ov = {o.x, o.y, o.z, o.w};
+    reinterpret_cast<b4*>(y16)[i] = __builtin_convertvector(ov, b4);
+  }
+}
 }  // namespace mdemi
+
+extern "C" int mdemi_add16(const float* a, const float* b, float* y, void* y16, int64_t n, void* stream) {
+  MDEMI_REQUIRE(a && b && y && y16 && n >= 0 && n % 4 == 0, "add16: bad args (n %% 4 == 0)");
+  MDEMI_REQUIRE(((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+                    ((uintptr_t)y16 & 7) == 0, "add16: misaligned operand");
+  if (n == 0) return MDEMI_OK;
+  int64_t nb = cdiv(n / 4, 256);
+  nb = nb < 16384 ? nb : 16384;
+  hipLaunchKernelGGL(add16_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const float4*)a,
+                     (const float4*)b, (float4*)y, (__bf16*)y16, n / 4);
+  return check_launch("add16");
+}
 
 extern "C" int mdemi_cast_bf16(const float* x, void* y, int64_t n, void* stream) {
   MDEMI_REQUIRE(x && y && n >= 0, "cast_bf16: bad args");

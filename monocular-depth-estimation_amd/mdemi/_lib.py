@@ -122,6 +122,12 @@ _SIGS = {
     "mdemi_gemm_bf16x_supported": (ctypes.c_int, [ctypes.POINTER(GemmDesc), vp, vp]),
     "mdemi_gemm_set_variant_b16": (ctypes.c_int, [i32]),
     "mdemi_cast_bf16": (ctypes.c_int, [vp, vp, i64, vp]),
+    "mdemi_add16": (ctypes.c_int, [vp, vp, vp, vp, i64, vp]),
+    "mdemi_bn_train_fwd16": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i64, i32, f32, i32, vp,
+                                            vp]),
+    "mdemi_chnorm_bwd16": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32,
+                                          vp, vp]),
+    "mdemi_chan_scale16": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i64, i32, vp]),
     "mdemi_gemm_set_options": (ctypes.c_int, [i32, i32]),
     "mdemi_colsum_workspace_size": (sz, [i64, i64]),
     "mdemi_colsum_f32": (ctypes.c_int, [vp, i64, i64, i64, vp, ctypes.c_int, vp, vp]),

@@ -115,32 +115,53 @@ def get_bf16_storage() -> bool:
     return _B16_STORAGE[0]
 
 
+# Parameters change in place through raw pointers (FusedAdamW's kernel), which torch's version
+# counter does not see: their bf16 copies are valid for one weight epoch, bumped by every
+# optimizer step (bump_weight_epoch), so each weight is cast once per train step and its copy
+# shared by the forward product and the data gradient.
+_W_EPOCH = [0]
+
+
+def bump_weight_epoch() -> None:
+    _W_EPOCH[0] += 1
+
+
 def set_b16(t, b16):
     """Record b16 (a bf16 tensor, t's shape, contiguous) as the RNE bf16 copy of t; valid
-    while t is not modified in place (t._version)."""
-    t._mdemi_b16 = (b16, t._version)
+    while t is not modified in place (t._version; parameters: for this weight epoch)."""
+    t._mdemi_b16 = (b16, t._version, _W_EPOCH[0])
     return t
 
 
-def b16_of(t, convert=True):
-    """The bf16 copy of contiguous fp32 tensor t: the recorded one (set_b16) if still valid,
-    else (convert) a cast sweep, recorded on t unless t is a parameter (updated in place by the
-    optimizer through raw pointers, which torch's version counter does not see).  None for a
-    tensor that cannot be copied this way (non-contiguous, unaligned)."""
+def _b16_rec(t, numel):
     rec = t.__dict__.get("_mdemi_b16")
-    if rec is not None and rec[1] == t._version and rec[0].numel() == t.numel():
-        return rec[0]
+    if rec is None or rec[1] != t._version or rec[0].numel() != numel:
+        return None
+    if t.is_leaf and t.requires_grad and rec[2] != _W_EPOCH[0]:
+        return None
+    return rec[0]
+
+
+def b16_of(t, convert=True):
+    """The bf16 copy of contiguous fp32 tensor t: the recorded one (set_b16; on t or on the
+    tensor t is a whole view of) if still valid, else (convert) a cast sweep, recorded on t --
+    or on the parameter t views.  None for a tensor that cannot be copied this way
+    (non-contiguous, unaligned)."""
+    b = _b16_rec(t, t.numel())
+    if b is not None:
+        return b
     base = t._base
-    if base is not None and base.data_ptr() == t.data_ptr() and base.numel() == t.numel():
-        rec = base.__dict__.get("_mdemi_b16")
-        if rec is not None and rec[1] == base._version and rec[0].numel() == t.numel():
-            return rec[0]
+    whole = base is not None and base.data_ptr() == t.data_ptr() and base.numel() == t.numel()
+    if whole:
+        b = _b16_rec(base, t.numel())
+        if b is not None:
+            return b.view(t.shape)
     if not convert or not t.is_contiguous() or t.data_ptr() % 16 or t.dtype != torch.float32:
         return None
     b = torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
     L.call("mdemi_cast_bf16", t.data_ptr(), b.data_ptr(), t.numel(), L.stream())
-    if not (t.is_leaf and t.requires_grad):
-        set_b16(t, b)
+    set_b16(base if (whole and base.is_contiguous()) else t, b if not (whole and base.is_contiguous())
+            else b.view(base.shape))
     return b
 
 
@@ -165,6 +186,11 @@ class matmul_precision:
     def __exit__(self, *a):
         set_matmul_precision(self.prev)
         return False
+
+
+# the path the last gemm() call took ("b16": bf16 operands in HBM; else the precision) -- for
+# the benchmark's per-family roofline, which prices bf16 operands at 2 bytes
+LAST_GEMM = ["fp32"]
 
 
 def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE, b_op=L.OP_NONE,
@@ -228,6 +254,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
             if need:
                 ws = L.workspace(need, C.device, slot=1)
                 d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+    LAST_GEMM[0] = "b16" if (a16 is not None and b16 is not None) else _PRECISION[0]
     if a16 is not None or b16 is not None or c16 is not None:
         if _PRECISION[0] != "bf16":
             raise ValueError("gemm: bf16 operands / output (a16, b16, c16) need matmul precision 'bf16'")
@@ -1047,15 +1074,21 @@ def nhwc_to_nchw(x):
 
 class _ChNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, groups, is_bn, eps, act, running=None):
+    def forward(ctx, x, weight, bias, groups, is_bn, eps, act, running=None, out_b16=False):
         """running: (running_mean, running_var, num_batches_tracked or None, momentum) -- the
-        BatchNorm running-statistics update done by the same call (mdemi_bn_train_fwd)."""
+        BatchNorm running-statistics update done by the same call (mdemi_bn_train_fwd).
+        out_b16: the output feeds a bf16 GEMM -- write its bf16 copy too (bf16 storage).  The
+        input gradient gets its bf16 copy when the input came from a conv (its data- and
+        weight-gradient GEMMs read it)."""
         _require_cuda(x, weight, bias)
         x = _c(x)
         n = x.shape[0]
         c = x.shape[-1]
         hw = x[0].numel() // c
         y = torch.empty_like(x)
+        y16 = new_b16_like(y) if (out_b16 and running is not None and is_bn) else None
+        ctx.dx16 = bool(is_bn and _PRECISION[0] == "bf16" and _B16_STORAGE[0] and x.grad_fn is not None
+                        and type(x.grad_fn).__name__ == "_Conv2dFnBackward")
         nstat = c if is_bn else n * groups
         mean = torch.empty(nstat, device=x.device, dtype=torch.float32)
         rstd = torch.empty(nstat, device=x.device, dtype=torch.float32)
@@ -1063,10 +1096,12 @@ class _ChNormFn(torch.autograd.Function):
         ws = L.workspace(lib.mdemi_chnorm_workspace_size(n, hw, c, groups, int(is_bn)), x.device)
         if running is not None:
             rm, rv, tracked, momentum = running
-            L.check(lib.mdemi_bn_train_fwd(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
-                                           mean.data_ptr(), rstd.data_ptr(), rm.data_ptr(), rv.data_ptr(),
-                                           L.ptr(tracked), float(momentum), n, hw, c, float(eps), act,
-                                           ws.data_ptr(), L.stream()), "bn_train_fwd")
+            L.check(lib.mdemi_bn_train_fwd16(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
+                                             L.ptr(y16), mean.data_ptr(), rstd.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+                                             L.ptr(tracked), float(momentum), n, hw, c, float(eps), act,
+                                             ws.data_ptr(), L.stream()), "bn_train_fwd")
+            if y16 is not None:
+                set_b16(y, y16)
         else:
             L.check(lib.mdemi_chnorm_fwd(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
                                          mean.data_ptr(), rstd.data_ptr(), n, hw, c, groups, int(is_bn), float(eps),
@@ -1080,7 +1115,7 @@ class _ChNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dm, _dr):
         if dy is None:
-            return None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, None
         x, weight, bias, mean, rstd = ctx.saved_tensors
         groups, is_bn, act = ctx.cfg
         dy = _c(dy)
@@ -1088,21 +1123,26 @@ class _ChNormFn(torch.autograd.Function):
         c = x.shape[-1]
         hw = x[0].numel() // c
         dx = torch.empty_like(x)
+        dx16 = new_b16_like(dx) if ctx.dx16 else None
         dg = torch.empty(c, device=x.device, dtype=torch.float32)
         db = torch.empty(c, device=x.device, dtype=torch.float32)
         lib = L.load()
         ws = L.workspace(lib.mdemi_chnorm_workspace_size(n, hw, c, groups, int(is_bn)), x.device)
-        L.check(lib.mdemi_chnorm_bwd(dy.data_ptr(), x.data_ptr(), None, mean.data_ptr(), rstd.data_ptr(),
-                                     weight.data_ptr(), bias.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(),
-                                     n, hw, c, groups, int(is_bn), act, ws.data_ptr(), L.stream()), "chnorm_bwd")
-        return dx, dg, db, None, None, None, None, None
+        L.check(lib.mdemi_chnorm_bwd16(dy.data_ptr(), x.data_ptr(), None, mean.data_ptr(), rstd.data_ptr(),
+                                       weight.data_ptr(), bias.data_ptr(), dx.data_ptr(), L.ptr(dx16), dg.data_ptr(),
+                                       db.data_ptr(), n, hw, c, groups, int(is_bn), act, ws.data_ptr(), L.stream()),
+                "chnorm_bwd")
+        if dx16 is not None:
+            set_b16(dx, dx16)
+        return dx, dg, db, None, None, None, None, None, None
 
 
-def batch_norm_nhwc(x, weight, bias, eps=1e-5, act=L.ACT_NONE, running=None):
+def batch_norm_nhwc(x, weight, bias, eps=1e-5, act=L.ACT_NONE, running=None, out_b16=False):
     """Training-mode BatchNorm2d over an NHWC map; returns (y, batch_mean, batch_rstd).
     running=(running_mean, running_var, num_batches_tracked or None, momentum) also applies
-    nn.BatchNorm2d's running-statistics update in the same call."""
-    return _ChNormFn.apply(x, weight, bias, x.shape[-1], True, eps, act, running)
+    nn.BatchNorm2d's running-statistics update in the same call.  out_b16: y feeds a bf16
+    GEMM (bf16 storage: its bf16 copy is written by the same sweep)."""
+    return _ChNormFn.apply(x, weight, bias, x.shape[-1], True, eps, act, running, out_b16)
 
 
 def group_norm_nhwc(x, weight, bias, groups, eps=1e-5, act=L.ACT_NONE):
@@ -1143,21 +1183,28 @@ def sigmoid_scale(x, s=1.0):
 
 class _AddFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b):
+    def forward(ctx, a, b, out_b16):
         _require_cuda(a, b)
         a, b = _c(a), _c(b)
         y = torch.empty_like(a)
-        L.call("mdemi_elementwise", L.EW_ADD, a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), 0.0, 0.0,
-               L.stream())
+        y16 = new_b16_like(y) if (out_b16 and y.numel() % 4 == 0 and a.data_ptr() % 16 == 0
+                                  and b.data_ptr() % 16 == 0) else None
+        if y16 is not None:
+            L.call("mdemi_add16", a.data_ptr(), b.data_ptr(), y.data_ptr(), y16.data_ptr(), a.numel(), L.stream())
+            set_b16(y, y16)
+        else:
+            L.call("mdemi_elementwise", L.EW_ADD, a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), 0.0, 0.0,
+                   L.stream())
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return dy, dy
+        return dy, dy, None
 
 
-def add(a, b):
-    return _AddFn.apply(a, b)
+def add(a, b, out_b16=False):
+    """a + b; out_b16: the sum feeds a bf16 GEMM (bf16 storage: its bf16 copy in the same sweep)."""
+    return _AddFn.apply(a, b, out_b16)
 
 
 # --------------------------------------------------------------------------
@@ -1396,11 +1443,14 @@ def spatial_reduce(a, b=None, scale=1.0):
     return out
 
 
-def _chan_scale(x, g, add=None):
+def _chan_scale(x, g, add=None, out_b16=False):
     y = torch.empty_like(x)
     n, c = x.shape[0], x.shape[-1]
-    L.call("mdemi_chan_scale", x.data_ptr(), g.data_ptr(), L.ptr(add), y.data_ptr(), n, x[0].numel() // c, c,
-           L.stream())
+    y16 = new_b16_like(y) if out_b16 else None
+    L.call("mdemi_chan_scale16", x.data_ptr(), g.data_ptr(), L.ptr(add), y.data_ptr(), L.ptr(y16), n,
+           x[0].numel() // c, c, L.stream())
+    if y16 is not None:
+        set_b16(y, y16)
     return y
 
 
@@ -1441,7 +1491,7 @@ class _SqueezeExciteFn(torch.autograd.Function):
         gate = torch.empty(n, c, device=x.device, dtype=torch.float32)
         L.call("mdemi_se_gate_fwd", pooled.data_ptr(), _c(wr).data_ptr(), br.data_ptr(), _c(we).data_ptr(),
                be.data_ptr(), hid.data_ptr(), gate.data_ptr(), n, c, r, L.stream())
-        y = _chan_scale(x, gate)
+        y = _chan_scale(x, gate, out_b16=True)  # SqueezeExcite's output feeds the projection conv
         ctx.save_for_backward(x, wr, we, pooled, hid, gate)
         return y
 

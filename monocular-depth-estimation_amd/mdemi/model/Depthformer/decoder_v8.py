@@ -63,6 +63,8 @@ class DepthFormerDecoderV8(nn.Module):
             ConvBN(self.hidden_dim * 5 // 8, self.hidden_dim, 3, act_layer=act_layer, use_residual=False),
             ConvBN(self.hidden_dim, self.hidden_dim, 3, act_layer=act_layer, use_residual=False),
             nn.Conv2d(self.hidden_dim, self.num_bins, kernel_size=(1, 1)))
+        self.bin_predictor[0].bn._mdemi_out_b16 = True  # both feed a conv (bf16 storage)
+        self.bin_predictor[1].bn._mdemi_out_b16 = True
         self._act = L.ACT_SILU if act_layer is nn.SiLU else None
         if self._act is None:
             raise NotImplementedError("DepthFormerDecoderV8 runs with its default act_layer=nn.SiLU")

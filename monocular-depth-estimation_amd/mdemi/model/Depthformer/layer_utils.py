@@ -56,6 +56,8 @@ class ResConvBNBlock(nn.Module):
                                  act_layer=act_layer if (i != num_layers - 1) else None, use_residual=False))
             channels = out_channels
         self.layers = nn.ModuleList(layers)
+        for layer in layers[:-1]:  # each but the last feeds the next layer's conv (bf16 storage)
+            layer.bn._mdemi_out_b16 = True
         self.use_residual = (in_channels == out_channels)
         if not self.use_residual:
             self.shortcut = ConvBN(in_channels, out_channels, kernel_size=1, act_layer=None, use_residual=False)
@@ -67,7 +69,7 @@ class ResConvBNBlock(nn.Module):
         for layer in self.layers:
             x = layer(x)
         identity = self.shortcut(identity) if not self.use_residual else identity
-        return mf.add(x, identity)
+        return mf.add(x, identity, out_b16=True)  # feeds the 1x1 shoot conv (decoder_v8.py:136)
 
 
 class UpscaleConcatAct(nn.Module):

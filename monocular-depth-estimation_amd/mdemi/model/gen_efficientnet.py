@@ -104,7 +104,8 @@ class SqueezeExcite(nn.Module):
 
 
 def _residual(x, shortcut):
-    return mf.add(x, shortcut)
+    # the block output feeds the next block's conv_pw (a bf16 GEMM under bf16 storage)
+    return mf.add(x, shortcut, out_b16=True)
 
 
 class DepthwiseSeparableConv(nn.Module):
@@ -119,6 +120,7 @@ class DepthwiseSeparableConv(nn.Module):
         self.se = SqueezeExcite(in_chs, in_chs)
         self.conv_pw = Conv2dSame(in_chs, out_chs, 1)
         self.bn2 = BatchNormAct2d(out_chs, act=False)
+        self.bn2._mdemi_out_b16 = not self.has_residual  # the block output feeds the next conv_pw
         self.act2 = nn.Identity()
 
     def forward(self, x):
@@ -142,6 +144,7 @@ class InvertedResidual(nn.Module):
         self.se = SqueezeExcite(mid, in_chs)
         self.conv_pwl = Conv2dSame(mid, out_chs, 1)
         self.bn3 = BatchNormAct2d(out_chs, act=False)
+        self.bn3._mdemi_out_b16 = not self.has_residual  # the block output feeds the next conv_pw
 
     def forward(self, x):
         y = self.bn2(self.conv_dw(self.bn1(self.conv_pw(x))))

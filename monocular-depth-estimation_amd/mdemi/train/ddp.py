@@ -188,3 +188,5 @@ def broadcast_parameters(model, src: int = 0, group=None):
     with torch.no_grad():
         for t in model.state_dict().values():
             dist.broadcast(t, src, group=group)
+    from .. import functional as mf
+    mf.bump_weight_epoch()  # the collective wrote the parameters: any bf16 copy is stale

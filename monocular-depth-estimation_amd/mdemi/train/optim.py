@@ -146,6 +146,10 @@ class FusedAdamW:
         params = self._with_grad()
         if not params:
             return
+        # the update writes the parameters through raw pointers: bf16 copies made before it
+        # (functional.b16_of) are stale from here on
+        from .. import functional as _mf
+        _mf.bump_weight_epoch()
         capturing = torch.cuda.is_current_stream_capturing()
         dev = torch.device("cuda", torch.cuda.current_device())
         lib = L.load()

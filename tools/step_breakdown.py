@@ -31,7 +31,7 @@ print(f"{steps} timed steps: wall {span / steps / 1e6:.2f} ms/step, kernel busy 
       f"{len(win) / steps:.0f} launches/step")
 fam = collections.defaultdict(float)
 for name, (d, n) in by.items():
-    key = "gemm" if ("gemm_f32_kernel" in name or "gemm_glds_kernel" in name) else ("winattn" if "winattn" in name else name)
+    key = "gemm" if any(g in name for g in ("gemm_f32_kernel", "gemm_glds_kernel", "gemm_m16_kernel", "gemm_b16_kernel")) else ("winattn" if "winattn" in name else name)
     fam[key] += d
 print("families (ms/step):", ", ".join(f"{k} {v / steps / 1e6:.2f}"
                                        for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:14]))
