@@ -281,11 +281,14 @@ def measure_files(args, trainer, pipe, B, world):
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    t0 = time.perf_counter()  # front end alone: decode (workers) + pinned H2D + augment sweep
-    for _ in range(args.steps):
+    # front end alone: decode (workers) + pinned H2D + augment sweep, over more batches than the
+    # workers hold prefetched (workers x prefetch_factor), so the rate is the decode rate
+    nfe = max(args.steps, 6 * max(pipe.workers, 1) * 4)
+    t0 = time.perf_counter()
+    for _ in range(nfe):
         pipe.next()
     torch.cuda.synchronize()
-    fe = time.perf_counter() - t0
+    fe = (time.perf_counter() - t0) * args.steps / nfe
     return {"images_per_sec": round(B * na * world * args.steps / elapsed, 3),
             "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "front_end_alone_images_per_sec": round(B * na * args.steps / fe, 2),
