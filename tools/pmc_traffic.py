@@ -13,14 +13,16 @@ template-argument prefix `gemm_f32_kernel<A, B, AOP, BOP,` that bench.py's
 roofline names, so whichever family dominates a run finds its traffic.  The fp32 family's
 two kernel templates -- register-staged gemm_f32_kernel<A, B, AOP, BOP, ...> and the
 direct-to-LDS gemm_glds_kernel<A, B, ...> (no load-time op) -- are one family, keyed
-`gemm_f32<A, B, AOP, BOP>`: the per-shape autotuner picks among them."""
+`gemm_f32<A, B, AOP, BOP>`: the per-shape autotuner picks among them.  The bf16-operand
+kernel (gemm_b16_kernel<AL, BL, BMT, OCC>, gemm_b16_kernel.h) is keyed by its
+`gemm_b16_kernel<AL, BL,` prefix, covering both row-tile variants."""
 import csv
 import json
 import re
 import sys
 
 FAMILY = re.compile(r"gemm_f32_kernel<\d+, \d+, \d+, \d+,|gemm_glds_kernel<\d+, \d+,|"
-                    r"gemm_m16_kernel<\d+, \d+, \d+, \d+, \d+,|winattn_\w+_kernel|binhead_nhwc_\w+")
+                    r"gemm_m16_kernel<\d+, \d+, \d+, \d+, \d+,|gemm_b16_kernel<\d+, \d+,|winattn_\w+_kernel|binhead_nhwc_\w+")
 F32 = re.compile(r"gemm_f32_kernel<(\d+), (\d+), (\d+), (\d+),")
 GLDS = re.compile(r"gemm_glds_kernel<(\d+), (\d+),")
 
