@@ -466,6 +466,22 @@ int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
                          const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
                          int32_t* step_dev, int32_t* tensor_steps, const float* sumsq, float max_norm,
                          float grad_scale, int64_t nitems, void* workspace, void* stream);
+/* The same two steps, also writing the RNE bf16 copy of every updated parameter t whose
+ * param16_dev[t] (a device array of ntensors pointers, entries may be null) is set: the
+ * bf16 operand its GEMMs read under bf16 storage (mdemi_gemm_bf16x), bit-identical to
+ * mdemi_cast_bf16 of the new values -- no per-weight cast sweep in the next forward.
+ * Replaces the per-step weight casts of autocast's bf16 weight cache
+ * (depthformer_v8.py:46-75 under torch.autocast; configs[4]). */
+int mdemi_adamw_step16(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
+                       const mdemi_adamw_group* groups_host, int32_t ngroups,
+                       const float* sumsq, float max_norm, float grad_scale, int32_t step,
+                       int32_t* tensor_steps, int64_t nitems, void* const* param16_dev, void* workspace,
+                       void* stream);
+int mdemi_adamw_step_dev16(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
+                           const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
+                           int32_t* step_dev, int32_t* tensor_steps, const float* sumsq, float max_norm,
+                           float grad_scale, int64_t nitems, void* const* param16_dev, void* workspace,
+                           void* stream);
 
 #ifdef __cplusplus
 }

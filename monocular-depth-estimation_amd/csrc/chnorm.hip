@@ -5,6 +5,8 @@
 // uper_crf_head.py:35 — the PPM's num_groups=256 override).
 // Variance is the biased batch variance used for normalisation (ATen
 // semantics); the unbiased value for running_var is derived by the caller.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace mdemi {
@@ -195,13 +197,17 @@ __global__ __launch_bounds__(CN_THREADS) void gn_bwd_kernel(const float* __restr
 }
 
 // ---------------------------------------------------------------------------
-// BatchNorm over NHWC with C % 4 == 0 (every BN layer of the hot path): float4
-// channel quads.  A block covers a contiguous run of rows; when C/4 < 256 the
-// block's threads are split into RPT = 256 / (C/4) row lanes that stride the
-// run together (all 256 threads busy for the 24..176-channel EfficientNet
-// maps), partials are combined through LDS and written per block; a second
-// kernel sums the block partials per channel in fp64 (64 channels x 4 lanes per
-// block).  Elementwise passes are float4 with 32-bit quad indices.
+// BatchNorm over NHWC with C % 4 == 0 (every BN layer of the hot path): channel
+// slices x row chunks.  The channels split into nsl slices of sq <= 64 float4
+// quads (<= 256 channels: a whole row, or a 1-KiB run of it); a block owns one
+// slice of one chunk of rows and its 256 threads are rpt = 256 / sq row lanes x sq
+// quads (a wave reads the runs of 64 / sq consecutive rows).  Each thread sweeps
+// its rows with the quad's per-channel parameters in registers -- no per-element
+// index division -- and keeps U rows' loads in flight per step; every accumulator
+// still takes its rows in order.  Statistics: each block writes fp32 partials of
+// its chunk per channel; bn_reduce4 sums them in fp64, one wave per channel quad
+// (64 lanes x U chunk loads in flight, then a fixed butterfly), so the combine is
+// one round trip instead of a serial walk over the chunks.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float4 f4(float v) { return make_float4(v, v, v, v); }
 typedef __bf16 cn_bf16x4_t __attribute__((ext_vector_type(4)));
@@ -213,90 +219,84 @@ __device__ __forceinline__ void store_bf16x4(__bf16* p, float4 o) {
 }
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// PASS 0: sum x; PASS 1: sum (x - mean)^2; PASS 2 (backward): (sum d*xhat, sum d) with
-// d = dy * act'(pre), pre = xhat * gamma + beta recomputed.  part: [blk][NV][C].
-// ACT >= 0: the activation fixed at compile time (no per-element switch); -1: runtime `act`.
-template <int PASS, int ACT = -1>
-__global__ __launch_bounds__(CN_THREADS) void bn_partial4(const float* __restrict__ x, const float* __restrict__ dy,
-                                                          const float* __restrict__ mean,
-                                                          const float* __restrict__ rstd,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float* __restrict__ part,
-                                                          int64_t rows, int C, int act, int64_t rows_per_blk) {
-  constexpr int NV = PASS == 2 ? 2 : 1;
-  __shared__ float4 red[NV][CN_THREADS];
-  if (ACT >= 0) act = ACT;
-  const int CQ = C >> 2, tid = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
-  const int64_t r1 = min(rows, r0 + rows_per_blk);
-  const int rpt = CQ >= CN_THREADS ? 1 : CN_THREADS / CQ;
-  const int lane_r = CQ >= CN_THREADS ? 0 : tid / CQ;
-  for (int cbase = 0; cbase < CQ; cbase += CN_THREADS) {
-    const int c4 = CQ >= CN_THREADS ? cbase + tid : tid % CQ;
-    const bool active = c4 < CQ && lane_r < rpt;
-    float4 s0 = f4(0.f), s1 = f4(0.f);
-    if (active) {
-      const int c = 4 * c4;
-      const float4 mu = PASS ? ld4(mean + c) : f4(0.f);
-      float4 rs = f4(1.f), ga = f4(1.f), be = f4(0.f);
-      if (PASS == 2) { rs = ld4(rstd + c); ga = ld4(gamma + c); be = ld4(beta + c); }
-      // unrolled so several rows' loads are in flight per thread; each accumulator still
-      // takes the rows in order (bit-identical to the rolled loop)
-#pragma unroll 4
-      for (int64_t r = r0 + lane_r; r < r1; r += rpt) {
-        const float4 v = ld4(x + r * C + c);
-        if (PASS == 0) {
-          s0.x += v.x; s0.y += v.y; s0.z += v.z; s0.w += v.w;
-        } else if (PASS == 1) {
-          const float4 u = make_float4(v.x - mu.x, v.y - mu.y, v.z - mu.z, v.w - mu.w);
-          s0.x = fmaf(u.x, u.x, s0.x); s0.y = fmaf(u.y, u.y, s0.y);
-          s0.z = fmaf(u.z, u.z, s0.z); s0.w = fmaf(u.w, u.w, s0.w);
-        } else {
-          const float4 g = ld4(dy + r * C + c);
-#define MDEMI_BNB(X)                                                  \
-  {                                                                    \
-    const float xh = (v.X - mu.X) * rs.X, pre = xh * ga.X + be.X;      \
-    const float d = g.X * act_grad(act, pre, apply_act(act, pre));     \
-    s0.X = fmaf(d, xh, s0.X);                                          \
-    s1.X += d;                                                         \
+constexpr int BN_SLICE_QUADS = 64;
+struct BnGrid {
+  int64_t rows, rpc;  // rows (N*H*W), rows per chunk
+  int C, CQ, nsl, sq, nchunk;
+};
+// nsl * nchunk ~= target blocks, chunks of >= 32 rows
+static BnGrid bn_grid(int64_t rows, int C, int target_blocks) {
+  BnGrid g;
+  g.rows = rows;
+  g.C = C;
+  g.CQ = C / 4;
+  g.nsl = (int)cdiv(g.CQ, BN_SLICE_QUADS);
+  g.sq = (int)cdiv(g.CQ, g.nsl);
+  int64_t nch = cdiv(target_blocks, g.nsl);
+  nch = nch < cdiv(rows, 32) ? nch : cdiv(rows, 32);
+  if (nch < 1) nch = 1;
+  g.rpc = cdiv(rows, nch);
+  g.nchunk = (int)cdiv(rows, g.rpc);
+  return g;
+}
+
+struct BnLane {
+  int64_t r0, r1;
+  int q, sq, lane_r, rpt, sl, chunk;
+};
+__device__ __forceinline__ BnLane bn_lane(const BnGrid& g) {
+  BnLane L;
+  L.sl = blockIdx.x % g.nsl;
+  L.chunk = blockIdx.x / g.nsl;
+  const int q0 = L.sl * g.sq;
+  L.sq = min(g.sq, g.CQ - q0);
+  L.rpt = CN_THREADS / L.sq;
+  L.lane_r = threadIdx.x / L.sq;
+  L.q = q0 + threadIdx.x % L.sq;
+  L.r0 = (int64_t)L.chunk * g.rpc;
+  L.r1 = min(g.rows, L.r0 + g.rpc);
+  return L;
+}
+// rows of this thread: r0 + lane_r, + rpt, ... < r1 (none for the idle lanes past rpt * sq)
+__device__ __forceinline__ int bn_lane_rows(const BnLane& L) {
+  const int64_t f = L.r0 + L.lane_r;
+  return (L.lane_r < L.rpt && f < L.r1) ? (int)((L.r1 - f + L.rpt - 1) / L.rpt) : 0;
+}
+
+// PASS 0 (forward): (sum x, sum x^2); PASS 2 (backward): (sum d*xhat, sum d) with
+// d = dy * act'(pre), pre = xhat * gamma + beta recomputed in fp32 as the apply does.
+// Sums are fp64 from the first element: x^2 of an fp32 x is exact in fp64, so the one-pass
+// variance sum x^2 / n - mean^2 keeps >= 53 - log2(mean^2 / var) bits -- more than the fp32
+// two-pass form it replaced for any activation with mean^2 / var < 2^29 -- and the
+// statistics are the correctly rounded values whatever the partition, for one read of x
+// instead of two.
+struct D4 {
+  double x, y, z, w;
+};
+__device__ __forceinline__ D4 d4zero() { return D4{0.0, 0.0, 0.0, 0.0}; }
+__device__ __forceinline__ void d4add(D4& s, const D4& a) { s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w; }
+template <int PASS>
+__device__ __forceinline__ void bn_acc(int act, float4 v, float4 g, float4 mu, float4 rs, float4 ga, float4 be,
+                                       D4& s0, D4& s1) {
+  if (PASS == 0) {
+    s0.x += (double)v.x; s0.y += (double)v.y; s0.z += (double)v.z; s0.w += (double)v.w;
+    s1.x = fma((double)v.x, (double)v.x, s1.x); s1.y = fma((double)v.y, (double)v.y, s1.y);
+    s1.z = fma((double)v.z, (double)v.z, s1.z); s1.w = fma((double)v.w, (double)v.w, s1.w);
+  } else {
+#define MDEMI_BNB(X)                                              \
+  {                                                                \
+    const float xh = (v.X - mu.X) * rs.X, pre = xh * ga.X + be.X;  \
+    const float d = g.X * act_grad(act, pre, apply_act(act, pre)); \
+    s0.X = fma((double)d, (double)xh, s0.X);                       \
+    s1.X += (double)d;                                             \
   }
-          MDEMI_BNB(x) MDEMI_BNB(y) MDEMI_BNB(z) MDEMI_BNB(w)
+    MDEMI_BNB(x) MDEMI_BNB(y) MDEMI_BNB(z) MDEMI_BNB(w)
 #undef MDEMI_BNB
-        }
-      }
-    }
-    if (rpt > 1) {  // combine the row lanes of each channel quad
-      red[0][tid] = s0;
-      if (NV == 2) red[NV - 1][tid] = s1;
-      __syncthreads();
-      if (tid < CQ) {
-        for (int k = 1; k < rpt; ++k) {
-          const float4 a = red[0][k * CQ + tid];
-          s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-          if (NV == 2) {
-            const float4 b = red[NV - 1][k * CQ + tid];
-            s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
-          }
-        }
-      }
-    }
-    if (rpt > 1 ? tid < CQ : active) {
-      float* dst = part + (int64_t)blockIdx.x * NV * C + 4 * c4;
-      *reinterpret_cast<float4*>(dst) = s0;
-      if (NV == 2) *reinterpret_cast<float4*>(dst + C) = s1;
-    }
-    if (rpt > 1) break;  // one pass covers every quad
   }
 }
 
-// fp64 sum of the block partials: a block owns CPB = min(C, 16) channels and
-// splits the partial rows over 256 / CPB lanes per channel, each lane keeping
-// four independent accumulators (memory-level parallelism over the strided
-// partial rows), then folds lanes and accumulators in a fixed order.
-// MODE 0: mean = s / rows; MODE 1: rstd = 1 / sqrt(s / rows + eps);
-// MODE 2: (dgamma, dbeta) from [blk][2][C].
-// nn.BatchNorm2d's running-statistics update (unbiased batch variance, momentum m), done by
-// the rstd combine when rmean is set: one launch fewer per training-mode BN
+// nn.BatchNorm2d's running-statistics update (unbiased batch variance, momentum m), done
+// with the rstd statistics: no separate launch per training-mode BN
 struct BnRunning {
   float* rmean;
   float* rvar;
@@ -309,50 +309,151 @@ __device__ __forceinline__ void bn_running_one(const BnRunning& run, float mu, f
   run.rvar[c] = (1.f - run.m) * run.rvar[c] + run.m * var;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256) void bn_combine4(const float* __restrict__ part, int nblk, int C, int64_t rows,
-                                                   float eps, float* __restrict__ out0, float* __restrict__ out1,
-                                                   BnRunning run = BnRunning{}, const float* __restrict__ mean = nullptr) {
-  constexpr int NV = MODE == 2 ? 2 : 1;
-  __shared__ double red[NV][256];
-  const int cpb = C < 16 ? C : 16, lpc = 256 / cpb;
-  const int cl = threadIdx.x % cpb, g = threadIdx.x / cpb;
-  const int c = blockIdx.x * cpb + cl;
-  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
-  if (c < C && g < lpc) {
-    const int64_t stride = (int64_t)NV * C;
-    int i = g;
-    for (; i + 3 * lpc < nblk; i += 4 * lpc) {
+// where the statistics go: MODE 0 (out0, out1) = (mean, rstd) (+ the running update);
+// MODE 2 (out0, out1) = (dgamma, dbeta).
+struct BnStatOut {
+  float* out0;
+  float* out1;
+  const float* mean;
+  float eps;
+  BnRunning run;
+};
+
+// fp64 sums of the chunk partials [chunk][2][C] (fp64): block b owns channel quad b;
+// thread t sums chunks t, t + 256, ... in order, the waves fold by a fixed xor butterfly
+// and the four wave sums add in wave order -- one round trip of loads per thread.
+__device__ __forceinline__ D4 ldd4(const double* p) {
+  const double2 a = *reinterpret_cast<const double2*>(p), b = *reinterpret_cast<const double2*>(p + 2);
+  return D4{a.x, a.y, b.x, b.y};
+}
+__device__ __forceinline__ void std4(double* p, const D4& v) {
+  *reinterpret_cast<double2*>(p) = make_double2(v.x, v.y);
+  *reinterpret_cast<double2*>(p + 2) = make_double2(v.z, v.w);
+}
+__device__ __forceinline__ void d4_wave_sum(D4& a) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a[u] += (double)part[(int64_t)(i + u * lpc) * stride + c];
-        if (NV == 2) b[u] += (double)part[(int64_t)(i + u * lpc) * stride + C + c];
-      }
+  for (int m = 32; m >= 1; m >>= 1) {
+    a.x += __shfl_xor(a.x, m, 64); a.y += __shfl_xor(a.y, m, 64);
+    a.z += __shfl_xor(a.z, m, 64); a.w += __shfl_xor(a.w, m, 64);
+  }
+}
+// MODE 0 (forward): mean = s / n, rstd = 1 / sqrt(q / n - mean^2 + eps) from (s, q) = (sum x,
+// sum x^2), plus the running update; MODE 2 (backward): (dgamma, dbeta).
+template <int MODE>
+__global__ __launch_bounds__(CN_THREADS) void bn_reduce4(const double* __restrict__ part, BnGrid g, BnStatOut o) {
+  constexpr int U = 4;
+  __shared__ D4 red[2][CN_THREADS / 64];
+  const int q = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = 4 * q;
+  D4 a = d4zero(), b = d4zero();
+  const int64_t stride = 2 * (int64_t)g.C, pstep = CN_THREADS * stride;
+  const double* p = part + (int64_t)threadIdx.x * stride + c;
+  const int n = (int)threadIdx.x < g.nchunk ? (g.nchunk - (int)threadIdx.x + CN_THREADS - 1) / CN_THREADS : 0;
+  int i = 0;
+  for (; i + U <= n; i += U) {
+    D4 va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      va[u] = ldd4(p + u * pstep);
+      vb[u] = ldd4(p + u * pstep + g.C);
     }
-    for (; i < nblk; i += lpc) {
-      a[0] += (double)part[(int64_t)i * stride + c];
-      if (NV == 2) b[0] += (double)part[(int64_t)i * stride + C + c];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      d4add(a, va[u]);
+      d4add(b, vb[u]);
+    }
+    p += U * pstep;
+  }
+  for (; i < n; ++i, p += pstep) {
+    d4add(a, ldd4(p));
+    d4add(b, ldd4(p + g.C));
+  }
+  d4_wave_sum(a);
+  d4_wave_sum(b);
+  if (lane == 0) {
+    red[0][w] = a;
+    red[1][w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  a = red[0][0];
+  b = red[1][0];
+  for (int k = 1; k < CN_THREADS / 64; ++k) {
+    d4add(a, red[0][k]);
+    d4add(b, red[1][k]);
+  }
+  if (MODE == 0 && o.run.tracked && q == 0) o.run.tracked[0] += 1;
+  const double sa[4] = {a.x, a.y, a.z, a.w}, sb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int cc = c + e;
+    if (MODE == 0) {
+      const double m = sa[e] / (double)g.rows, var = fmax(sb[e] / (double)g.rows - m * m, 0.0);
+      const float mf = (float)m, r = (float)(1.0 / sqrt(var + (double)o.eps));
+      o.out0[cc] = mf;
+      o.out1[cc] = r;
+      if (o.run.rmean) bn_running_one(o.run, mf, r, o.eps, cc);
+    } else {
+      o.out0[cc] = (float)sa[e];
+      o.out1[cc] = (float)sb[e];
     }
   }
-  if (MODE == 1 && run.tracked && blockIdx.x == 0 && threadIdx.x == 0) run.tracked[0] += 1;
-  red[0][threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
-  if (NV == 2) red[NV - 1][threadIdx.x] = (b[0] + b[1]) + (b[2] + b[3]);
+}
+
+// statistics sweep of one (slice, chunk) block: its fp64 partials to part[chunk][NV][C].
+// ACT >= 0: the activation fixed at compile time (no per-element switch); -1: runtime `act`.
+template <int PASS, int ACT = -1>
+__global__ __launch_bounds__(CN_THREADS) void bn_stats4(const float* __restrict__ x, const float* __restrict__ dy,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, double* __restrict__ part,
+                                                        BnGrid g, int act) {
+  constexpr int NV = 2;
+  constexpr int U = 8;
+  __shared__ D4 red[NV * CN_THREADS];
+  if (ACT >= 0) act = ACT;
+  const BnLane L = bn_lane(g);
+  const int n = bn_lane_rows(L), c = 4 * L.q;
+  D4 s0 = d4zero(), s1 = d4zero();
+  if (n > 0) {
+    const float4 mu = PASS == 2 ? ld4(mean + c) : f4(0.f);
+    float4 rs = f4(1.f), ga = f4(1.f), be = f4(0.f);
+    if (PASS == 2) { rs = ld4(rstd + c); ga = ld4(gamma + c); be = ld4(beta + c); }
+    const int64_t step = (int64_t)L.rpt * g.C, base = (L.r0 + L.lane_r) * g.C + c;
+    const float* px = x + base;
+    const float* pg = dy + (PASS == 2 ? base : 0);
+    int i = 0;
+    for (; i + U <= n; i += U) {
+      float4 v[U], gv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = ld4(px + u * step);
+        gv[u] = PASS == 2 ? ld4(pg + u * step) : f4(0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) bn_acc<PASS>(act, v[u], gv[u], mu, rs, ga, be, s0, s1);
+      px += U * step;
+      if (PASS == 2) pg += U * step;
+    }
+    for (; i < n; ++i) {
+      bn_acc<PASS>(act, ld4(px), PASS == 2 ? ld4(pg) : f4(0.f), mu, rs, ga, be, s0, s1);
+      px += step;
+      if (PASS == 2) pg += step;
+    }
+  }
+  // fold the row lanes of each quad in lane order (rpt >= 4: sq <= 64)
+  red[threadIdx.x] = s0;
+  if (NV == 2) red[CN_THREADS + threadIdx.x] = s1;
   __syncthreads();
-  if (g == 0 && c < C) {
-    double sa = 0.0, sb = 0.0;
-    for (int k = 0; k < lpc; ++k) {
-      sa += red[0][k * cpb + cl];
-      if (NV == 2) sb += red[NV - 1][k * cpb + cl];
+  if ((int)threadIdx.x < L.sq) {
+    for (int k = 1; k < L.rpt; ++k) {
+      d4add(s0, red[k * L.sq + threadIdx.x]);
+      if (NV == 2) d4add(s1, red[CN_THREADS + k * L.sq + threadIdx.x]);
     }
-    if (MODE == 0) out0[c] = (float)(sa / (double)rows);
-    else if (MODE == 1) {
-      const float r = (float)(1.0 / sqrt(sa / (double)rows + (double)eps));
-      out0[c] = r;
-      if (run.rmean) bn_running_one(run, mean[c], r, eps, c);
-    } else {
-      out0[c] = (float)sa;
-      out1[c] = (float)sb;
-    }
+    double* dst = part + (int64_t)L.chunk * NV * g.C + c;
+    std4(dst, s0);
+    if (NV == 2) std4(dst + g.C, s1);
   }
 }
 
@@ -360,21 +461,34 @@ template <int ACT = -1>
 __global__ __launch_bounds__(CN_THREADS) void bn_apply4(const float* __restrict__ x, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, float* __restrict__ y,
-                                                        int64_t total4, int CQ, int act,
-                                                        __bf16* __restrict__ y16 = nullptr) {
+                                                        __bf16* __restrict__ y16, BnGrid g, int act) {
+  constexpr int U = 4;
   if (ACT >= 0) act = ACT;
-  for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
-    const int c = 4 * (int)(e % CQ);
-    const float4 v = reinterpret_cast<const float4*>(x)[e];
-    const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
-    float4 o;
-    o.x = apply_act(act, (v.x - mu.x) * rs.x * ga.x + be.x);
-    o.y = apply_act(act, (v.y - mu.y) * rs.y * ga.y + be.y);
-    o.z = apply_act(act, (v.z - mu.z) * rs.z * ga.z + be.z);
-    o.w = apply_act(act, (v.w - mu.w) * rs.w * ga.w + be.w);
-    reinterpret_cast<float4*>(y)[e] = o;
-    if (y16) store_bf16x4(y16 + 4 * e, o);
+  const BnLane L = bn_lane(g);
+  const int n = bn_lane_rows(L), c = 4 * L.q;
+  if (n == 0) return;
+  const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
+  const int64_t step = (int64_t)L.rpt * g.C;
+  int64_t off = (L.r0 + L.lane_r) * g.C + c;
+  auto one = [&](float4 v, int64_t o) {
+    float4 r;
+    r.x = apply_act(act, (v.x - mu.x) * rs.x * ga.x + be.x);
+    r.y = apply_act(act, (v.y - mu.y) * rs.y * ga.y + be.y);
+    r.z = apply_act(act, (v.z - mu.z) * rs.z * ga.z + be.z);
+    r.w = apply_act(act, (v.w - mu.w) * rs.w * ga.w + be.w);
+    *reinterpret_cast<float4*>(y + o) = r;
+    if (y16) store_bf16x4(y16 + o, r);
+  };
+  int i = 0;
+  for (; i + U <= n; i += U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld4(x + off + u * step);
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(v[u], off + u * step);
+    off += U * step;
   }
+  for (; i < n; ++i, off += step) one(ld4(x + off), off);
 }
 
 template <int ACT = -1>
@@ -385,35 +499,58 @@ __global__ __launch_bounds__(CN_THREADS) void bn_bwd_apply4(const float* __restr
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ dgamma,
                                                             const float* __restrict__ dbeta, float* __restrict__ dx,
-                                                            int64_t total4, int CQ, float inv_n, int act,
-                                                            __bf16* __restrict__ dx16 = nullptr) {
+                                                            __bf16* __restrict__ dx16, BnGrid g, float inv_n, int act) {
+  constexpr int U = 4;
   if (ACT >= 0) act = ACT;
-  for (int64_t e = (int64_t)blockIdx.x * CN_THREADS + threadIdx.x; e < total4; e += (int64_t)gridDim.x * CN_THREADS) {
-    const int c = 4 * (int)(e % CQ);
-    const float4 v = reinterpret_cast<const float4*>(x)[e];
-    const float4 g = reinterpret_cast<const float4*>(dy)[e];
-    const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
-    const float4 dg = ld4(dgamma + c), db = ld4(dbeta + c);
-    float4 o;
-#define MDEMI_BNA(X)                                                                  \
-  {                                                                                    \
-    const float xh = (v.X - mu.X) * rs.X, pre = xh * ga.X + be.X;                      \
-    const float d = g.X * act_grad(act, pre, apply_act(act, pre));                     \
-    o.X = ga.X * rs.X * (d - inv_n * db.X - xh * inv_n * dg.X);                         \
+  const BnLane L = bn_lane(g);
+  const int n = bn_lane_rows(L), c = 4 * L.q;
+  if (n == 0) return;
+  const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
+  const float4 dg = ld4(dgamma + c), db = ld4(dbeta + c);
+  const int64_t step = (int64_t)L.rpt * g.C;
+  int64_t off = (L.r0 + L.lane_r) * g.C + c;
+  auto one = [&](float4 v, float4 gr, int64_t o) {
+    float4 r;
+#define MDEMI_BNA(X)                                                              \
+  {                                                                                \
+    const float xh = (v.X - mu.X) * rs.X, pre = xh * ga.X + be.X;                  \
+    const float d = gr.X * act_grad(act, pre, apply_act(act, pre));                \
+    r.X = ga.X * rs.X * (d - inv_n * db.X - xh * inv_n * dg.X);                     \
   }
     MDEMI_BNA(x) MDEMI_BNA(y) MDEMI_BNA(z) MDEMI_BNA(w)
 #undef MDEMI_BNA
-    reinterpret_cast<float4*>(dx)[e] = o;
-    if (dx16) store_bf16x4(dx16 + 4 * e, o);
+    *reinterpret_cast<float4*>(dx + o) = r;
+    if (dx16) store_bf16x4(dx16 + o, r);
+  };
+  int i = 0;
+  for (; i + U <= n; i += U) {
+    float4 v[U], gr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = ld4(x + off + u * step);
+      gr[u] = ld4(dy + off + u * step);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(v[u], gr[u], off + u * step);
+    off += U * step;
   }
+  for (; i < n; ++i, off += step) one(ld4(x + off), ld4(dy + off), off);
 }
 
-// blocks for the vectorised path: enough to fill the chip, >= 16 rows each
-static int bn4_blocks(int64_t rows) {
-  int64_t nb = cdiv(rows, 16);
-  return (int)(nb > 1024 ? 1024 : (nb < 1 ? 1 : nb));
+// block targets of the statistics and elementwise sweeps (tunable for A/B runs)
+static int env_blocks(const char* name, int dflt) {
+  const char* s = getenv(name);
+  const int v = s ? atoi(s) : 0;
+  return v > 0 ? v : dflt;
 }
-static unsigned bn4_combine_grid(int C) { return (unsigned)cdiv(C, C < 16 ? C : 16); }
+static int bn_stat_blocks() {
+  static const int v = env_blocks("MDEMI_BN_STAT_BLOCKS", 1024);
+  return v;
+}
+static int bn_apply_blocks() {
+  static const int v = env_blocks("MDEMI_BN_APPLY_BLOCKS", 2048);
+  return v;
+}
 
 static int rows_per_block(int64_t rows) {
   // ~256 partial blocks
@@ -441,15 +578,17 @@ using namespace mdemi;
   }
 #define MDEMI_KT_APPLY4(A) bn_apply4<A>
 #define MDEMI_KT_BWDAPPLY4(A) bn_bwd_apply4<A>
-#define MDEMI_KT_PARTIAL4_2(A) bn_partial4<2, A>
+#define MDEMI_KT_STATS4_2(A) bn_stats4<2, A>
 
 extern "C" size_t mdemi_chnorm_workspace_size(int32_t N, int64_t HW, int32_t C, int32_t groups, int32_t is_bn) {
   (void)groups;
   if (is_bn) {
     const int64_t rows = (int64_t)N * HW;
     const int64_t nblk = cdiv(rows, rows_per_block(rows));
-    const int64_t nb4 = bn4_blocks(rows);
-    return (size_t)(nblk > nb4 ? nblk : nb4) * 2 * C * sizeof(float);
+    const int64_t nb4 = C % 4 == 0 ? bn_grid(rows, C, bn_stat_blocks()).nchunk : 0;
+    // fp32 partials of the scalar path, fp64 ones of the vector path (bn_stats4)
+    const size_t a = (size_t)nblk * 2 * C * sizeof(float), b = (size_t)nb4 * 2 * C * sizeof(double);
+    return a > b ? a : b;
   }
   return (size_t)N * 2 * C * sizeof(float);
 }
@@ -475,22 +614,16 @@ static int chnorm_fwd_impl(const float* x, const float* gamma, const float* beta
     const int64_t rows = (int64_t)N * HW;
     float* part = (float*)workspace;
     if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
-      const int nb = bn4_blocks(rows);
-      const int64_t rpb4 = cdiv(rows, nb);
-      const unsigned cg = bn4_combine_grid(C);
-      // two passes (mean, then the centred sum of squares): a one-pass Welford/Chan form saved
-      // a read of x but moved the statistics by rounding, enough to flip kink- and
-      // cancellation-sensitive parity tests; kept two-pass
-      hipLaunchKernelGGL(bn_partial4<0>, dim3(nb), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma, beta, part,
-                         rows, C, act, rpb4);
-      hipLaunchKernelGGL(bn_combine4<0>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, mean, nullptr);
-      hipLaunchKernelGGL(bn_partial4<1>, dim3(nb), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma, beta, part,
-                         rows, C, act, rpb4);
-      hipLaunchKernelGGL(bn_combine4<1>, dim3(cg), dim3(256), 0, st, part, nb, C, rows, eps, rstd, nullptr, run,
-                         (const float*)mean);
-      const int64_t total4 = rows * C / 4;
-      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_APPLY4, act, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, x, gamma, beta, mean,
-                          rstd, y, total4, C / 4, act, y16);
+      const BnGrid gs = bn_grid(rows, C, bn_stat_blocks()), ga = bn_grid(rows, C, bn_apply_blocks());
+      // one read of x for the statistics: (sum x, sum x^2) in fp64 (the round-4 one-pass form
+      // kept fp32 Welford state and moved mean / rstd enough to flip ill-conditioned parity
+      // tests; fp64 sums do not -- DESIGN.md §5)
+      const BnStatOut o0{mean, rstd, nullptr, eps, run};
+      hipLaunchKernelGGL(bn_stats4<0>, dim3(gs.nsl * gs.nchunk), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma,
+                         beta, (double*)part, gs, act);
+      hipLaunchKernelGGL(bn_reduce4<0>, dim3(gs.CQ), dim3(CN_THREADS), 0, st, (const double*)part, gs, o0);
+      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_APPLY4, act, dim3(ga.nsl * ga.nchunk), dim3(CN_THREADS), 0, st, x, gamma, beta, mean,
+                          rstd, y, y16, ga, act);
       return check_launch("chnorm_fwd");
     }
     const int rpb = rows_per_block(rows);
@@ -575,15 +708,14 @@ extern "C" int mdemi_chnorm_bwd16(const float* dy, const float* x, const float* 
   if (is_bn) {
     const int64_t rows = (int64_t)N * HW;
     if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
-      const int nb = bn4_blocks(rows);
-      const int64_t rpb4 = cdiv(rows, nb);
-      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_PARTIAL4_2, act, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta,
-                          part, rows, C, act, rpb4);
-      hipLaunchKernelGGL(bn_combine4<2>, dim3(bn4_combine_grid(C)), dim3(256), 0, st, part, nb, C, rows, 0.f, dgamma,
-                         dbeta);
-      const int64_t total4 = rows * C / 4;
-      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_BWDAPPLY4, act, dim3(grid_for(total4)), dim3(CN_THREADS), 0, st, dy, x, mean, rstd,
-                          gamma, beta, dgamma, dbeta, dx, total4, C / 4, 1.f / (float)rows, act, dx16);
+      const BnGrid gs = bn_grid(rows, C, bn_stat_blocks()), ga = bn_grid(rows, C, bn_apply_blocks());
+      const BnStatOut o2{dgamma, dbeta, nullptr, 0.f, BnRunning{}};
+      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_STATS4_2, act, dim3(gs.nsl * gs.nchunk), dim3(CN_THREADS), 0, st, x, dy, mean, rstd,
+                          gamma, beta, (double*)part, gs, act);
+      hipLaunchKernelGGL(bn_reduce4<2>, dim3(gs.CQ), dim3(CN_THREADS), 0, st, (const double*)part, gs,
+                         o2);
+      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_BWDAPPLY4, act, dim3(ga.nsl * ga.nchunk), dim3(CN_THREADS), 0, st, dy, x, mean, rstd,
+                          gamma, beta, dgamma, dbeta, dx, dx16, ga, 1.f / (float)rows, act);
       return check_launch("chnorm_bwd");
     }
     const int rpb = rows_per_block(rows);
@@ -618,7 +750,7 @@ extern "C" int mdemi_chnorm_apply(const float* x, const float* gamma, const floa
 // Backward of the inference-mode normalisation (BatchNorm2d in eval mode inside a
 // training step, e.g. a frozen encoder's BN): mean / rstd are constants, so
 // dx = gamma * rstd * act'(pre) * dy with no batch terms; dgamma / dbeta are the same
-// channel sums as in training (bn_partial4<2> / bn_bwd_partial).
+// channel sums as in training (bn_stats4<2> / bn_bwd_partial).
 __global__ __launch_bounds__(CN_THREADS) void bn_frozen_dx(const float* __restrict__ dy, const float* __restrict__ x,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
@@ -669,11 +801,12 @@ extern "C" int mdemi_bn_frozen_bwd(const float* dy, const float* x, const float*
     if (!workspace) { set_error("bn_frozen_bwd: workspace required"); return MDEMI_EWORKSPACE; }
     float* part = (float*)workspace;
     if (vec) {
-      const int nb = bn4_blocks(rows);
-      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_PARTIAL4_2, act, dim3(nb), dim3(CN_THREADS), 0, st, x, dy, mean, rstd, gamma, beta,
-                          part, rows, C, act, cdiv(rows, nb));
-      hipLaunchKernelGGL(bn_combine4<2>, dim3(bn4_combine_grid(C)), dim3(256), 0, st, part, nb, C, rows, 0.f, dgamma,
-                         dbeta);
+      const BnGrid gs = bn_grid(rows, C, bn_stat_blocks());
+      const BnStatOut o2{dgamma, dbeta, nullptr, 0.f, BnRunning{}};
+      MDEMI_BN_ACT_LAUNCH(MDEMI_KT_STATS4_2, act, dim3(gs.nsl * gs.nchunk), dim3(CN_THREADS), 0, st, x, dy, mean, rstd,
+                          gamma, beta, (double*)part, gs, act);
+      hipLaunchKernelGGL(bn_reduce4<2>, dim3(gs.CQ), dim3(CN_THREADS), 0, st, (const double*)part, gs,
+                         o2);
     } else {
       const int rpb = rows_per_block(rows);
       const int nblk = (int)cdiv(rows, rpb);

@@ -168,6 +168,25 @@ __global__ __launch_bounds__(256) void dropout_dev_kernel(const float* __restric
     y[i] = uniform01(seed, offset + (uint64_t)i) >= p ? x[i] * inv_keep : 0.f;
 }
 
+// float4 form (n % 4 == 0, 16-B aligned): the same mask element for element, four hashes
+// per thread and one 16-B load / store -- the scalar form reached ~45 % of HBM
+__global__ __launch_bounds__(256) void dropout_dev4_kernel(const float4* __restrict__ x, float4* __restrict__ y,
+                                                           int64_t n4, float p, float inv_keep,
+                                                           const uint64_t* __restrict__ seed_dev, uint64_t seed_add,
+                                                           uint64_t offset) {
+  const uint64_t seed = seed_dev[0] + seed_add;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
+    const float4 v = x[e];
+    const uint64_t i = offset + 4 * (uint64_t)e;
+    float4 o;
+    o.x = uniform01(seed, i) >= p ? v.x * inv_keep : 0.f;
+    o.y = uniform01(seed, i + 1) >= p ? v.y * inv_keep : 0.f;
+    o.z = uniform01(seed, i + 2) >= p ? v.z * inv_keep : 0.f;
+    o.w = uniform01(seed, i + 3) >= p ? v.w * inv_keep : 0.f;
+    y[e] = o;
+  }
+}
+
 __global__ __launch_bounds__(256) void act_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
                                                       int act) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
@@ -608,8 +627,15 @@ extern "C" int mdemi_dropout(const float* x, float* y, int64_t n, float p, uint6
 extern "C" int mdemi_dropout_dev(const float* x, float* y, int64_t n, float p, const uint64_t* seed_dev,
                                  uint64_t seed_add, uint64_t offset, void* stream) {
   MDEMI_REQUIRE(x && y && n > 0 && p > 0.f && p < 1.f && seed_dev, "dropout_dev: bad args");
-  hipLaunchKernelGGL(dropout_dev_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, p,
-                     1.f / (1.f - p), seed_dev, seed_add, offset);
+  if (n % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    const int64_t n4 = n / 4;
+    const unsigned g = (unsigned)std::min<int64_t>(cdiv(n4, 256), 8192);
+    hipLaunchKernelGGL(dropout_dev4_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float4*)x, (float4*)y,
+                       n4, p, 1.f / (1.f - p), seed_dev, seed_add, offset);
+  } else {
+    hipLaunchKernelGGL(dropout_dev_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, p,
+                       1.f / (1.f - p), seed_dev, seed_add, offset);
+  }
   return check_launch("dropout_dev");
 }
 

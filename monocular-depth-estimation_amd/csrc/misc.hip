@@ -177,8 +177,13 @@ __global__ void sumsq_final(const float* __restrict__ part, int nitems, float* _
 
 // torch.optim.AdamW on one (tensor, chunk) item (decoupled weight decay,
 // non-amsgrad, foreach=False semantics); `step` is the 1-based step count
+// p16 (optional): also write the RNE bf16 copy of the updated parameter -- the operand
+// its bf16 GEMMs read next step (what mdemi_cast_bf16 would produce, bit for bit)
+typedef __bf16 opt_bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float opt_f32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void adamw_item(const mdemi_tensor_ref& t, const mdemi_adamw_group& gp, float clip,
-                                           float gs, float step, int64_t beg, int64_t end) {
+                                           float gs, float step, int64_t beg, int64_t end,
+                                           __bf16* __restrict__ p16 = nullptr) {
   const float b1 = gp.beta1, b2 = gp.beta2;
   const float step_size = gp.lr / (1.f - powf(b1, step));
   const float bc2s = sqrtf(1.f - powf(b2, step));
@@ -191,7 +196,8 @@ __device__ __forceinline__ void adamw_item(const mdemi_tensor_ref& t, const mdem
     v = v * b2 + (1.f - b2) * g * g;
     p -= step_size * m / (sqrtf(v) / bc2s + gp.eps);
   };
-  const bool vec = (((uintptr_t)t.param | (uintptr_t)t.grad | (uintptr_t)t.exp_avg | (uintptr_t)t.exp_avg_sq) & 15) == 0;
+  const bool vec = (((uintptr_t)t.param | (uintptr_t)t.grad | (uintptr_t)t.exp_avg | (uintptr_t)t.exp_avg_sq) & 15) == 0 &&
+                   ((uintptr_t)p16 & 7) == 0;
   const int64_t vend = vec ? beg + ((end - beg) & ~(int64_t)3) : beg;
   for (int64_t i = beg + 4 * threadIdx.x; i < vend; i += 4 * OPT_THREADS) {
     const float4 g = *reinterpret_cast<const float4*>(t.grad + i);
@@ -202,8 +208,15 @@ __device__ __forceinline__ void adamw_item(const mdemi_tensor_ref& t, const mdem
     *reinterpret_cast<float4*>(t.param + i) = p;
     *reinterpret_cast<float4*>(t.exp_avg + i) = m;
     *reinterpret_cast<float4*>(t.exp_avg_sq + i) = v;
+    if (p16) {
+      const opt_f32x4_t pv = {p.x, p.y, p.z, p.w};
+      *reinterpret_cast<opt_bf16x4_t*>(p16 + i) = __builtin_convertvector(pv, opt_bf16x4_t);
+    }
   }
-  for (int64_t i = vend + threadIdx.x; i < end; i += OPT_THREADS) upd(t.grad[i], t.param[i], t.exp_avg[i], t.exp_avg_sq[i]);
+  for (int64_t i = vend + threadIdx.x; i < end; i += OPT_THREADS) {
+    upd(t.grad[i], t.param[i], t.exp_avg[i], t.exp_avg_sq[i]);
+    if (p16) p16[i] = (__bf16)t.param[i];
+  }
 }
 
 __device__ __forceinline__ float clip_coef(const float* sumsq, float max_norm) {
@@ -216,12 +229,15 @@ __global__ __launch_bounds__(OPT_THREADS) void adamw_kernel(const mdemi_tensor_r
                                                             const int* __restrict__ chunk_tensor,
                                                             const int* __restrict__ chunk_index, AdamGroups groups,
                                                             const float* __restrict__ sumsq, float max_norm, float gs,
-                                                            int step, const int* __restrict__ tensor_steps) {
+                                                            int step, const int* __restrict__ tensor_steps,
+                                                            void* const* __restrict__ p16tab) {
   const int item = blockIdx.x;
-  const mdemi_tensor_ref t = tl[chunk_tensor[item]];
+  const int ti = chunk_tensor[item];
+  const mdemi_tensor_ref t = tl[ti];
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
   const int s = tensor_steps ? tensor_steps[t.step_slot] + 1 : step;
-  adamw_item(t, groups.g[t.group], clip_coef(sumsq, max_norm), gs, (float)s, beg, min(t.numel, beg + OPT_CHUNK));
+  adamw_item(t, groups.g[t.group], clip_coef(sumsq, max_norm), gs, (float)s, beg, min(t.numel, beg + OPT_CHUNK),
+             p16tab ? (__bf16*)p16tab[ti] : nullptr);
 }
 
 // capturable form: hyperparameters of step s (= *step_dev, steps already taken)
@@ -234,14 +250,16 @@ __global__ __launch_bounds__(OPT_THREADS) void adamw_dev_kernel(const mdemi_tens
                                                                 const int* __restrict__ step_dev,
                                                                 const int* __restrict__ tensor_steps,
                                                                 const float* __restrict__ sumsq, float max_norm,
-                                                                float gs) {
+                                                                float gs, void* const* __restrict__ p16tab) {
   const int item = blockIdx.x;
-  const mdemi_tensor_ref t = tl[chunk_tensor[item]];
+  const int ti = chunk_tensor[item];
+  const mdemi_tensor_ref t = tl[ti];
   const int s = step_dev[0];
   const mdemi_adamw_group gp = sched[(int64_t)min(s, nsteps - 1) * ngroups + t.group];
   const int64_t beg = (int64_t)chunk_index[item] * OPT_CHUNK;
   const int bc = tensor_steps ? tensor_steps[t.step_slot] + 1 : s + 1;
-  adamw_item(t, gp, clip_coef(sumsq, max_norm), gs, (float)bc, beg, min(t.numel, beg + OPT_CHUNK));
+  adamw_item(t, gp, clip_coef(sumsq, max_norm), gs, (float)bc, beg, min(t.numel, beg + OPT_CHUNK),
+             p16tab ? (__bf16*)p16tab[ti] : nullptr);
 }
 
 // after the update: advance the optimizer's step counter and/or every listed
@@ -385,6 +403,14 @@ extern "C" int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t nte
                                 const mdemi_adamw_group* groups_host, int32_t ngroups, const float* sumsq,
                                 float max_norm, float grad_scale, int32_t step, int32_t* tensor_steps, int64_t nitems,
                                 void* workspace, void* stream) {
+  return mdemi_adamw_step16(tensors_dev, ntensors, groups_host, ngroups, sumsq, max_norm, grad_scale, step,
+                            tensor_steps, nitems, nullptr, workspace, stream);
+}
+
+extern "C" int mdemi_adamw_step16(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
+                                  const mdemi_adamw_group* groups_host, int32_t ngroups, const float* sumsq,
+                                  float max_norm, float grad_scale, int32_t step, int32_t* tensor_steps,
+                                  int64_t nitems, void* const* param16_dev, void* workspace, void* stream) {
   MDEMI_REQUIRE(tensors_dev && ntensors > 0 && groups_host && ngroups > 0 && ngroups <= 4 &&
                     (step >= 1 || tensor_steps) && nitems > 0 && workspace && grad_scale > 0.f,
                 "adamw_step: bad args");
@@ -395,7 +421,7 @@ extern "C" int mdemi_adamw_step(const mdemi_tensor_ref* tensors_dev, int32_t nte
   const int* ci = ct + nitems;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, st, tensors_dev, ct, ci, g, sumsq,
-                     max_norm, grad_scale, step, (const int*)tensor_steps);
+                     max_norm, grad_scale, step, (const int*)tensor_steps, param16_dev);
   if (tensor_steps)
     hipLaunchKernelGGL(step_tick_kernel, dim3((unsigned)cdiv(ntensors, 256)), dim3(256), 0, st, (int*)nullptr,
                        tensors_dev, ntensors, (int*)tensor_steps);
@@ -406,6 +432,15 @@ extern "C" int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t
                                     const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
                                     int32_t* step_dev, int32_t* tensor_steps, const float* sumsq, float max_norm,
                                     float grad_scale, int64_t nitems, void* workspace, void* stream) {
+  return mdemi_adamw_step_dev16(tensors_dev, ntensors, sched_dev, nsteps, ngroups, step_dev, tensor_steps, sumsq,
+                                max_norm, grad_scale, nitems, nullptr, workspace, stream);
+}
+
+extern "C" int mdemi_adamw_step_dev16(const mdemi_tensor_ref* tensors_dev, int32_t ntensors,
+                                      const mdemi_adamw_group* sched_dev, int32_t nsteps, int32_t ngroups,
+                                      int32_t* step_dev, int32_t* tensor_steps, const float* sumsq, float max_norm,
+                                      float grad_scale, int64_t nitems, void* const* param16_dev, void* workspace,
+                                      void* stream) {
   MDEMI_REQUIRE(tensors_dev && ntensors > 0 && sched_dev && nsteps > 0 && ngroups > 0 && ngroups <= 4 && step_dev &&
                     nitems > 0 && workspace && grad_scale > 0.f,
                 "adamw_step_dev: bad args");
@@ -413,7 +448,8 @@ extern "C" int mdemi_adamw_step_dev(const mdemi_tensor_ref* tensors_dev, int32_t
   const int* ci = ct + nitems;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(adamw_dev_kernel, dim3((unsigned)nitems), dim3(OPT_THREADS), 0, st, tensors_dev, ct, ci, sched_dev,
-                     nsteps, ngroups, (const int*)step_dev, (const int*)tensor_steps, sumsq, max_norm, grad_scale);
+                     nsteps, ngroups, (const int*)step_dev, (const int*)tensor_steps, sumsq, max_norm, grad_scale,
+                     param16_dev);
   hipLaunchKernelGGL(step_tick_kernel, dim3((unsigned)cdiv(ntensors, 256)), dim3(256), 0, st, (int*)step_dev,
                      tensors_dev, ntensors, (int*)tensor_steps);
   return check_launch("adamw_step_dev");

@@ -173,6 +173,9 @@ _SIGS = {
     "mdemi_grad_sumsq": (ctypes.c_int, [vp, i32, i64, f32, vp, vp, vp]),
     "mdemi_adamw_step": (ctypes.c_int, [vp, i32, ctypes.POINTER(AdamWGroup), i32, vp, f32, f32, i32, vp, i64, vp, vp]),
     "mdemi_adamw_step_dev": (ctypes.c_int, [vp, i32, vp, i32, i32, vp, vp, vp, f32, f32, i64, vp, vp]),
+    "mdemi_adamw_step16": (ctypes.c_int, [vp, i32, ctypes.POINTER(AdamWGroup), i32, vp, f32, f32, i32, vp, i64, vp, vp,
+                                          vp]),
+    "mdemi_adamw_step_dev16": (ctypes.c_int, [vp, i32, vp, i32, i32, vp, vp, vp, f32, f32, i64, vp, vp, vp]),
     # ---- include/mdemi_ext.h ----
     "mdemi_dwconv_fwd": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mdemi_dwconv_bwd_workspace_size": (sz, [i32, i32, i32, i32, i32]),

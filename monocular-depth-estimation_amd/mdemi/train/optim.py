@@ -71,6 +71,10 @@ class FusedAdamW:
         # tensors, a rebuilt pointer table): a captured graph recorded with an older
         # layout must be re-captured (Trainer checks)
         self.layout_version = 0
+        # parameter -> persistent bf16 copy the update also writes (mdemi_adamw_step16): kept
+        # for every parameter a bf16 GEMM has read (bf16 storage), so the next forward
+        # finds a valid copy instead of casting each weight again
+        self._b16 = {}
 
     # ---- capturable schedule ----
     def set_schedule(self, rows):
@@ -109,7 +113,7 @@ class FusedAdamW:
         return [p for g in self.param_groups for p in g["params"] if p.grad is not None]
 
     def _refs(self):
-        refs, items_t, items_c, slots = [], [], [], []
+        refs, items_t, items_c, slots, p16 = [], [], [], [], []
         for gi, g in enumerate(self.param_groups):
             for p in g["params"]:
                 if p.grad is None:
@@ -127,18 +131,22 @@ class FusedAdamW:
                 ti = len(refs)
                 refs.append(r)
                 slots.append(self._slot[p])
+                b16 = self._b16.get(p)
+                p16.append(b16.data_ptr() if b16 is not None else 0)
                 nch = max(1, math.ceil(p.numel() / self._chunk))
                 items_t.extend([ti] * nch)
                 items_c.extend(range(nch))
-        return refs, items_t, items_c, slots
+        return refs, items_t, items_c, slots, p16
 
     def _key(self, params):
         """Every address the pointer table holds: a param, its grad, its state."""
         key = []
         for p in params:
             st = self.state.get(p)
+            b16 = self._b16.get(p)
             key.append((p.data_ptr(), p.grad.data_ptr(),
-                        st["exp_avg"].data_ptr() if st else 0, st["exp_avg_sq"].data_ptr() if st else 0))
+                        st["exp_avg"].data_ptr() if st else 0, st["exp_avg_sq"].data_ptr() if st else 0,
+                        b16.data_ptr() if b16 is not None else 0))
         return tuple(key)
 
     @torch.no_grad()
@@ -149,6 +157,9 @@ class FusedAdamW:
         # the update writes the parameters through raw pointers: bf16 copies made before it
         # (functional.b16_of) are stale from here on
         from .. import functional as _mf
+        for p in params:  # parameters a bf16 GEMM read this step get a maintained bf16 copy
+            if p not in self._b16 and _mf._b16_rec(p, p.numel()) is not None:
+                self._b16[p] = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
         _mf.bump_weight_epoch()
         capturing = torch.cuda.is_current_stream_capturing()
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -161,20 +172,25 @@ class FusedAdamW:
             # inside a capture (gradients handed out by the captured backward) the upload is a
             # memcpy node from the pinned host table, which stays alive with the device copy:
             # every replay re-copies the same addresses
-            refs, items_t, items_c, slots = self._refs()
+            refs, items_t, items_c, slots, p16 = self._refs()
             nt, ni = len(refs), len(items_t)
             raw = (L.TensorRef * nt)(*refs)
             rb = (ctypes.sizeof(raw) + 255) // 256 * 256
+            pb = (8 * nt + 255) // 256 * 256 if any(p16) else 0  # bf16 copy pointers (mdemi_adamw_step16)
             wsb = lib.mdemi_grad_norm_workspace_size(ni)
-            host = torch.empty(rb + wsb, dtype=torch.uint8, pin_memory=True)
+            host = torch.empty(rb + pb + wsb, dtype=torch.uint8, pin_memory=True)
             ctypes.memmove(host.data_ptr(), ctypes.addressof(raw), ctypes.sizeof(raw))
-            host[rb:rb + 8 * ni].view(torch.int32).copy_(torch.tensor(items_t + items_c, dtype=torch.int32))
+            if pb:
+                host[rb:rb + 8 * nt].view(torch.int64).copy_(torch.tensor(p16, dtype=torch.int64))
+            w0 = rb + pb
+            host[w0:w0 + 8 * ni].view(torch.int32).copy_(torch.tensor(items_t + items_c, dtype=torch.int32))
             dev_buf = host.to(dev, non_blocking=True)
-            self._tbl = (host, dev_buf, dev_buf.data_ptr(), dev_buf.data_ptr() + rb, nt, ni)
+            self._tbl = (host, dev_buf, dev_buf.data_ptr(), dev_buf.data_ptr() + w0, nt, ni,
+                         dev_buf.data_ptr() + rb if pb else None)
             self._tbl_key = self._key(params)
             self._tbl_slots = slots
             self.layout_version += 1
-        _, _, tl_ptr, ws_ptr, nt, ni = self._tbl
+        _, _, tl_ptr, ws_ptr, nt, ni, p16_ptr = self._tbl
         if self._steps_dev is None:
             if capturing:
                 raise RuntimeError("FusedAdamW: step counters must exist before hipGraph capture")
@@ -188,16 +204,20 @@ class FusedAdamW:
         steps_ptr = self._steps_dev.data_ptr()
         if self.capturable:
             sched, nsteps = self._device_schedule(dev, self.step_count)
-            L.check(lib.mdemi_adamw_step_dev(tl_ptr, nt, sched.data_ptr(), nsteps, len(self.param_groups),
-                                             self._step_dev.data_ptr(), steps_ptr, clip, self.max_grad_norm, gs,
-                                             ni, ws_ptr, L.stream()), "adamw_step_dev")
+            L.check(lib.mdemi_adamw_step_dev16(tl_ptr, nt, sched.data_ptr(), nsteps, len(self.param_groups),
+                                               self._step_dev.data_ptr(), steps_ptr, clip, self.max_grad_norm, gs,
+                                               ni, p16_ptr, ws_ptr, L.stream()), "adamw_step_dev")
         else:
             groups = (L.AdamWGroup * len(self.param_groups))()
             for i, g in enumerate(self.param_groups):
                 groups[i].lr, (groups[i].beta1, groups[i].beta2) = g["lr"], g["betas"]
                 groups[i].eps, groups[i].weight_decay = g["eps"], g["weight_decay"]
-            L.check(lib.mdemi_adamw_step(tl_ptr, nt, groups, len(self.param_groups), clip, self.max_grad_norm, gs,
-                                         self.step_count + 1, steps_ptr, ni, ws_ptr, L.stream()), "adamw_step")
+            L.check(lib.mdemi_adamw_step16(tl_ptr, nt, groups, len(self.param_groups), clip, self.max_grad_norm, gs,
+                                           self.step_count + 1, steps_ptr, ni, p16_ptr, ws_ptr, L.stream()),
+                    "adamw_step")
+        for p, b16 in self._b16.items():  # the update wrote these copies at the new weight epoch
+            if p.grad is not None:
+                _mf.set_b16(p, b16)
         if not capturing:  # a capture records the step; replays advance the mirrors (replayed())
             self.replayed()
 

@@ -133,6 +133,36 @@ def test_dropout_mask_is_reproduced_in_backward(mf):
     assert mf.dropout(x, 0.1, False) is x
 
 
+def _uniform01_np(seed, ctr):
+    """heads.hip uniform01: splitmix64 of seed + golden * (ctr + 1), top 24 bits."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (ctr.astype(np.uint64) + np.uint64(1))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(40)).astype(np.float64) / 16777216.0
+
+
+@pytest.mark.parametrize("n,shift", [(4096, 0), (4099, 0), (4096, 1)])
+def test_dropout_dev_mask_matches_hash(mf, n, shift):
+    """mdemi_dropout_dev: the float4 form (n % 4 == 0, aligned) and the scalar form draw the
+    same mask, element for element, as the hash restated in numpy."""
+    import numpy as np
+    from mdemi import _lib as L
+    base = torch.randn(n + shift, device=DEV)
+    x = base[shift:]
+    y = torch.empty_like(x)
+    seed = torch.tensor([123456789], device=DEV, dtype=torch.int64)
+    L.call("mdemi_dropout_dev", x.data_ptr(), y.data_ptr(), n, 0.3, seed.data_ptr(), 5, 1000, L.stream())
+    torch.cuda.synchronize()
+    u = _uniform01_np(123456789 + 5, np.arange(n, dtype=np.uint64) + np.uint64(1000))
+    want = np.where(u >= np.float32(0.3), x.cpu().numpy() * np.float32(1 / 0.7), 0.0).astype(np.float32)
+    got = y.cpu().numpy()
+    assert np.array_equal(got != 0, want != 0)
+    np.testing.assert_allclose(got, want, rtol=1e-6)
+
+
 @pytest.mark.parametrize("B,H,W,K", [(2, 5, 7, 256), (1, 3, 4, 32), (3, 16, 20, 128), (2, 48, 64, 256),
                                      (1, 17, 23, 64), (2, 9, 31, 512), (1, 6, 6, 36)])
 def test_bin_head_nhwc(mf, B, H, W, K):

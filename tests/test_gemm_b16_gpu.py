@@ -222,3 +222,60 @@ def test_bf16_storage_step_matches_fp32_operand_step(mf, bn):
             assert torch.equal(g0[k], g1[k]), k
     print(f"bf16 storage step == fp32-operand bf16 step bit for bit; {n_bias} bias gradients reassociated "
           f"(worst relative L2 {worst})")
+
+
+def test_adamw_maintains_bf16_weight_copies(mf):
+    """Under bf16 storage FusedAdamW writes each GEMM weight's bf16 copy in the update
+    (mdemi_adamw_step16): after a step every maintained copy equals the RNE cast of the new
+    weights bit for bit and is the valid recorded copy, and the next forward casts no
+    parameter (only activations without a producer-written copy are cast)."""
+    from mdemi import _lib as L
+    from mdemi.model.Depthformer import DepthformerV8
+    from mdemi.train.optim import FusedAdamW
+    from oracle.weights import closed_form_fill, rng_array
+    opt = {"hidden_dim": 64, "num_heads": 4, "num_bins": 64, "num_aux": 32, "img_size": [128, 160],
+           "attn_drop_prob": 0.0, "drop_prob": 0.0}
+    torch.manual_seed(0)
+    m = DepthformerV8.build(opt, 1e-3, 10.0)
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    closed_form_fill(sd, seed=0.61, scale=0.03)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    img = torch.from_numpy(rng_array((2, 3, 128, 160), 31)).float().to(DEV)
+    dy = torch.from_numpy(rng_array((2, 1, 64, 80), 32)).float().to(DEV)
+    o = FusedAdamW(m.parameters(), lr=1e-4, weight_decay=1e-2, max_grad_norm=0.1)
+    ptrs = {p.data_ptr() for p in m.parameters()}
+    casts = []
+    real_call = L.call
+
+    def counting(name, *args):
+        if name == "mdemi_cast_bf16" and args[0] in ptrs:
+            casts.append(args[0])
+        return real_call(name, *args)
+
+    prev = mf.get_bf16_storage()
+    mf.set_bf16_storage(True)
+    try:
+        with mf.matmul_precision("bf16"):
+            for it in range(3):
+                casts.clear()
+                L.call = counting
+                try:
+                    depth, _, _ = m(img)
+                finally:
+                    L.call = real_call
+                (depth * dy).sum().backward()
+                o.step()
+                o.zero_grad()
+                if it == 0:
+                    n_first = len(casts)
+                else:
+                    assert not casts, (it, len(casts))
+                torch.cuda.synchronize()
+                assert o._b16, "no parameter got a maintained bf16 copy"
+                for p, b in o._b16.items():
+                    assert torch.equal(b, p.detach().to(torch.bfloat16))
+                    assert mf.b16_of(p, convert=False) is b
+    finally:
+        mf.set_bf16_storage(prev)
+    print(f"{len(o._b16)} weights kept in bf16 by the update; first forward cast {n_first}, later ones 0")

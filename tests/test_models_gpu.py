@@ -321,6 +321,7 @@ def _check_fwd_conditioned(name, got, r64, r32, slack=20.0, rel=1e-4):
     e_gpu = (got.double().cpu() - r64).abs().max().item()
     e_cpu = (r32.double() - r64).abs().max().item()
     mag = r64.abs().max().item()
+    print(f"{name}: gpu err {e_gpu:.3e} = {e_gpu / max(rel * mag, slack * e_cpu):.3f} of the bound (cpu fp32 err {e_cpu:.3e})")
     assert e_gpu <= max(rel * mag, slack * e_cpu) + 1e-9, (name, e_gpu, e_cpu, mag)
 
 
