@@ -50,12 +50,40 @@ def _split_for(M, N, K):
     # under bf16, whose workgroups finish a k-tile several times faster (bf16 Depthformer
     # 78.95 -> 77.44 ms; fp32 NeW-CRFs unchanged, AdaBins within noise; 128 slower again --
     # tools/gpu_r4r.sh, gpu_r4s.sh, profiles/round4/ab_split_min_rows.txt)
-    min_kt = _SPLIT_MIN_KTILES if get_matmul_precision() == "bf16" else 32
-    if tiles >= 384 or ktiles < min_kt:
+    bf16 = get_matmul_precision() == "bf16"
+    min_kt = _SPLIT_MIN_KTILES if bf16 else 32
+    if ktiles < min_kt:
+        return 1
+    # fp32 only: narrower outputs keep the deep splits they need; bf16 workgroups finish a
+    # k-tile several times faster, so there the slab combine dominates and the round-4 rule
+    # measured better (Depthformer bf16 140.3 vs 138.2 img/s, profiles/round5/ab_split_policy.txt)
+    if tiles >= 32 and not bf16 and _SPLIT_POLICY == "fill":
+        return _split_fill(tiles, min(ktiles // min_kt, 128), 1 if tiles >= 384 else min(
+            max(1, _target_blocks() // tiles), ktiles // min_kt, 128))
+    if tiles >= 384:
         return 1
     target, cap = (_target_blocks(), 128) if tiles >= 8 else (2 * _target_blocks(), 512)
     split = min(max(1, target // tiles), ktiles // min_kt, cap)
     return max(1, split)
+
+
+_SPLIT_POLICY = os.environ.get("MDEMI_SPLIT_POLICY", "fill")  # "legacy": the round-4 rule (A/B)
+
+
+def _split_fill(tiles, smax, s_legacy):
+    """Split factor by wave quantisation: the tiles x split workgroups run in rounds of one per
+    CU, so a split whose last round is nearly empty wastes that round (768x768x9600: 36 tiles x
+    18 = 648 workgroups = 2.5 rounds, 147 us; x 7 = 252 = one full round, 126 us).  Cost per
+    unit of work: rounds / split, times 1 % per split for the slab traffic and the last
+    arriver's serial combine (tools/gemm_split_study.py, profiles/round5/split_study.txt).  The
+    round-4 rule's factor stays unless this one is >= 5 % cheaper by the model."""
+    cus = 256
+
+    def cost(s):
+        return -(-tiles * s // cus) / s * (1.0 + 0.01 * s)
+
+    best = min(range(1, max(1, smax) + 1), key=lambda s: (cost(s), s))
+    return best if cost(best) < 0.95 * cost(s_legacy) else s_legacy
 
 
 _SPLIT_MIN_KTILES = int(os.environ.get("MDEMI_SPLIT_MIN_KTILES", "16"))  # bf16; K tiles of 16 rows

@@ -11,9 +11,11 @@ from mdemi import _lib as L  # noqa: E402
 from mdemi import functional as mf  # noqa: E402
 
 # (layout, M, N, K) from profiles/r02_gemm_shapes.txt
-SHAPES = [("dgrad", 9600, 768, 3072), ("dgrad", 9600, 768, 2304), ("dgrad", 9600, 768, 768),
-          ("wgrad", 3072, 768, 9600), ("wgrad", 2304, 768, 9600), ("wgrad", 768, 768, 9600),
-          ("wgrad", 768, 3072, 9600), ("dgrad", 2400, 1536, 6144), ("wgrad", 576, 192, 153600)]
+SHAPES = [("wgrad", 3072, 768, 9600), ("wgrad", 2304, 768, 9600), ("wgrad", 768, 768, 9600),
+          ("wgrad", 768, 3072, 9600), ("wgrad", 576, 192, 153600), ("wgrad", 768, 192, 153600),
+          ("wgrad", 192, 768, 153600), ("wgrad", 384, 1536, 38400), ("wgrad", 1536, 384, 38400),
+          ("wgrad", 192, 192, 153600), ("wgrad", 6144, 1536, 2400), ("dgrad", 2400, 1536, 6144)]
+CANDIDATES = [int(v) for v in os.environ.get("SPLITS", "1,2,3,4,5,6,7,8,10,12,14,16,18,24,28,36").split(",")]
 
 
 def run(lay, M, N, K, split):
@@ -39,7 +41,8 @@ def run(lay, M, N, K, split):
 
 for lay, M, N, K in SHAPES:
     cur = mf._split_for(M, N, K)
-    res = {sp: run(lay, M, N, K, sp) for sp in sorted({1, 2, 4, 8, cur, max(1, cur // 2), cur * 2})}
+    kt = -(-K // 16)
+    res = {sp: run(lay, M, N, K, sp) for sp in sorted({cur, *CANDIDATES, 2 * cur, 3 * cur}) if sp <= max(1, kt // 8)}
     best = min(res, key=res.get)
-    print(f"{lay} {M}x{N}x{K} heuristic split {cur}: " + " ".join(f"s{k}={v:.0f}us" for k, v in res.items())
-          + f"  best s{best}", flush=True)
+    print(f"{lay} {M}x{N}x{K} tiles {-(-M // 128) * -(-N // 128)} heuristic split {cur} ({res[cur]:.0f}us): "
+          + " ".join(f"s{k}={v:.0f}" for k, v in res.items()) + f"  best s{best} ({res[best]:.0f}us)", flush=True)
