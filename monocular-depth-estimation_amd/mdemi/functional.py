@@ -846,7 +846,18 @@ class _WindowAttnFn(torch.autograd.Function):
         if dv_t.shape[1] > C and not same:
             dv_t.zero_()
         d_rpb = torch.empty_like(rpb)
-        pad_g = torch.zeros(3, C, device=qk.device, dtype=torch.float32)
+        # the pad tokens' (q, k, v) gradients, which the kernel's scatter writes whole (dq: zeros):
+        # straight into the bias gradients where their layout allows (Swin qkv.bias [q|k|v];
+        # NeW-CRF qk.bias [q|k] with a bias-free v), else into a [3, C] scratch assembled below
+        dqk_bias = dv_bias = None
+        if ctx.has_qkb and same and ctx.has_vb and v_off == 2 * C and qk_bias.numel() == 3 * C:
+            dqk_bias = torch.empty_like(qk_bias)
+            pad_g = dqk_bias.view(3, C)
+        elif ctx.has_qkb and not same and not ctx.has_vb and qk_bias.numel() == 2 * C:
+            dqk_bias = torch.empty_like(qk_bias)
+            pad_g = (dqk_bias[:C], dqk_bias[C:], torch.empty(C, device=qk.device, dtype=torch.float32))
+        else:
+            pad_g = torch.empty(3, C, device=qk.device, dtype=torch.float32)
         d = L.WinAttnDesc()
         d.B, d.H, d.W, d.heads, d.head_dim, d.window, d.shift = B, H, W, heads, C // heads, window, shift
         d.scale = scale
@@ -867,8 +878,7 @@ class _WindowAttnFn(torch.autograd.Function):
         ws = L.workspace(need, qk.device)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
         L.check(lib.mdemi_winattn_bwd(ctypes.byref(d), L.stream()), "winattn_bwd")
-        dqk_bias = dv_bias = None
-        if ctx.has_qkb:
+        if ctx.has_qkb and dqk_bias is None:
             dqk_bias = torch.zeros_like(qk_bias)
             dqk_bias[:C] = pad_g[0]
             dqk_bias[C:2 * C] = pad_g[1]
