@@ -224,6 +224,11 @@ int mdemi_binhead_bwd(const float* logits, const float* centers, const float* pr
 int mdemi_layernorm_fwd(const float* x, const float* gamma, const float* beta,
                         float* y, float* mean, float* rstd, int64_t rows, int32_t C,
                         float eps, void* stream);
+/* The same, also writing y16 (optional, 8-B aligned): the RNE bf16 copy of y that a bf16
+ * GEMM reading the normalised rows takes as its operand (bf16 storage; luna_layer.py:202-250
+ * and feed_forward.py:29-46 under torch.autocast, configs[4]). */
+int mdemi_layernorm_fwd16(const float* x, const float* gamma, const float* beta, float* y, void* y16,
+                          float* mean, float* rstd, int64_t rows, int32_t C, float eps, void* stream);
 size_t mdemi_layernorm_bwd_workspace_size(int64_t rows, int32_t C);
 int mdemi_layernorm_bwd(const float* dy, const float* x, const float* mean,
                         const float* rstd, const float* gamma, float* dx,

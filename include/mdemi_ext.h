@@ -75,6 +75,12 @@ int mdemi_se_gate_bwd(const float* pooled, const float* wr, const float* we, con
 int mdemi_softmax_fwd(const float* x, float* y, int64_t rows, int32_t cols, float scale, void* stream);
 int mdemi_softmax_bwd(const float* y, const float* dy, float* dx, int64_t rows, int32_t cols, float scale,
                       int32_t accumulate, void* stream);
+/* The same two, also writing the RNE bf16 copy of the result (y16 / dx16, optional): the
+ * attention probabilities feed P.V and the score gradient feeds dQ / dK as bf16 GEMM operands
+ * (luna_layer.py:202-250 and self_attention.py:61-80 under torch.autocast, configs[4]). */
+int mdemi_softmax_fwd16(const float* x, float* y, void* y16, int64_t rows, int32_t cols, float scale, void* stream);
+int mdemi_softmax_bwd16(const float* y, const float* dy, float* dx, void* dx16, int64_t rows, int32_t cols,
+                        float scale, int32_t accumulate, void* stream);
 
 /* y = act(x) elementwise (MDEMI_ACT_* code): the standalone activations of
  * UpscaleConcatAct (layer_utils.py:121) and the bin regressor
@@ -91,6 +97,11 @@ int mdemi_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, u
  * hipGraph-captured train step gets a fresh mask on every replay. */
 int mdemi_dropout_dev(const float* x, float* y, int64_t n, float p, const uint64_t* seed_dev, uint64_t seed_add,
                       uint64_t offset, void* stream);
+/* The same mask, also writing y16 (optional; n % 4 == 0, 16-B aligned x / y, 8-B aligned
+ * y16): the RNE bf16 copy of y for a bf16 GEMM that reads it -- the dropout backward's
+ * gradient feeding the linear before it (luna_layer.py:172-173 under torch.autocast). */
+int mdemi_dropout_dev16(const float* x, float* y, void* y16, int64_t n, float p, const uint64_t* seed_dev,
+                        uint64_t seed_add, uint64_t offset, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Channels-last adaptive-bin head: logits [B][HW][K] (the 1x1 conv_out /    */

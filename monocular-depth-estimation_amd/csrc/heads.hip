@@ -29,8 +29,11 @@ static unsigned grid_1d(int64_t total, int per_block = 256) {
 // ---------------------------------------------------------------------------
 constexpr int SM_REG = 16;  // values per lane for the wave-per-row path
 
+// y16 / dx16 (optional): the RNE bf16 copy of the result, for the bf16 GEMM that reads it
+// (attention probabilities into P.V, the score gradient into dQ / dK; bf16 storage)
 __global__ __launch_bounds__(256) void softmax_wave_fwd(const float* __restrict__ x, float* __restrict__ y,
-                                                        int64_t rows, int cols, float scale) {
+                                                        int64_t rows, int cols, float scale,
+                                                        __bf16* __restrict__ y16) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -56,12 +59,15 @@ __global__ __launch_bounds__(256) void softmax_wave_fwd(const float* __restrict_
 #pragma unroll
   for (int i = 0; i < SM_REG; ++i) {
     const int c = lane + 64 * i;
-    if (c < cols) yr[c] = v[i] * inv;
+    if (c < cols) {
+      yr[c] = v[i] * inv;
+      if (y16) y16[row * cols + c] = (__bf16)(v[i] * inv);
+    }
   }
 }
 
 __global__ __launch_bounds__(256) void softmax_block_fwd(const float* __restrict__ x, float* __restrict__ y, int cols,
-                                                         float scale) {
+                                                         float scale, __bf16* __restrict__ y16) {
   __shared__ float red[8];
   const int64_t row = blockIdx.x;
   const float* xr = x + row * cols;
@@ -90,12 +96,16 @@ __global__ __launch_bounds__(256) void softmax_block_fwd(const float* __restrict
   for (int i = 0; i < 4; ++i) gs += red[4 + i] * __expf(red[i] - gm);
   const float inv = 1.f / gs;
   float* yr = y + row * cols;
-  for (int c = threadIdx.x; c < cols; c += 256) yr[c] = __expf(scale * xr[c] - gm) * inv;
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const float o = __expf(scale * xr[c] - gm) * inv;
+    yr[c] = o;
+    if (y16) y16[row * cols + c] = (__bf16)o;
+  }
 }
 
 __global__ __launch_bounds__(256) void softmax_wave_bwd(const float* __restrict__ y, const float* __restrict__ dy,
                                                         float* __restrict__ dx, int64_t rows, int cols, float scale,
-                                                        int accumulate) {
+                                                        int accumulate, __bf16* __restrict__ dx16) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -117,14 +127,16 @@ __global__ __launch_bounds__(256) void softmax_wave_bwd(const float* __restrict_
     const int c = lane + 64 * i;
     if (c < cols) {
       const float v = scale * yv[i] * (gv[i] - d);
-      xr[c] = accumulate ? xr[c] + v : v;
+      const float o = accumulate ? xr[c] + v : v;
+      xr[c] = o;
+      if (dx16) dx16[row * cols + c] = (__bf16)o;
     }
   }
 }
 
 __global__ __launch_bounds__(256) void softmax_block_bwd(const float* __restrict__ y, const float* __restrict__ dy,
                                                          float* __restrict__ dx, int cols, float scale,
-                                                         int accumulate) {
+                                                         int accumulate, __bf16* __restrict__ dx16) {
   __shared__ float red[4];
   const int64_t row = blockIdx.x;
   const float* yr = y + row * cols;
@@ -135,7 +147,9 @@ __global__ __launch_bounds__(256) void softmax_block_bwd(const float* __restrict
   float* xr = dx + row * cols;
   for (int c = threadIdx.x; c < cols; c += 256) {
     const float v = scale * yr[c] * (gr[c] - d);
-    xr[c] = accumulate ? xr[c] + v : v;
+    const float o = accumulate ? xr[c] + v : v;
+    xr[c] = o;
+    if (dx16) dx16[row * cols + c] = (__bf16)o;
   }
 }
 
@@ -170,10 +184,12 @@ __global__ __launch_bounds__(256) void dropout_dev_kernel(const float* __restric
 
 // float4 form (n % 4 == 0, 16-B aligned): the same mask element for element, four hashes
 // per thread and one 16-B load / store -- the scalar form reached ~45 % of HBM
+typedef __bf16 dp_bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float dp_f32x4_t __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void dropout_dev4_kernel(const float4* __restrict__ x, float4* __restrict__ y,
                                                            int64_t n4, float p, float inv_keep,
                                                            const uint64_t* __restrict__ seed_dev, uint64_t seed_add,
-                                                           uint64_t offset) {
+                                                           uint64_t offset, dp_bf16x4_t* __restrict__ y16) {
   const uint64_t seed = seed_dev[0] + seed_add;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
     const float4 v = x[e];
@@ -184,6 +200,10 @@ __global__ __launch_bounds__(256) void dropout_dev4_kernel(const float4* __restr
     o.z = uniform01(seed, i + 2) >= p ? v.z * inv_keep : 0.f;
     o.w = uniform01(seed, i + 3) >= p ? v.w * inv_keep : 0.f;
     y[e] = o;
+    if (y16) {
+      const dp_f32x4_t ov = {o.x, o.y, o.z, o.w};
+      y16[e] = __builtin_convertvector(ov, dp_bf16x4_t);
+    }
   }
 }
 
@@ -588,24 +608,36 @@ static int metrics_chunks(int64_t HW) {
 using namespace mdemi;
 
 extern "C" int mdemi_softmax_fwd(const float* x, float* y, int64_t rows, int32_t cols, float scale, void* stream) {
+  return mdemi_softmax_fwd16(x, y, nullptr, rows, cols, scale, stream);
+}
+
+extern "C" int mdemi_softmax_fwd16(const float* x, float* y, void* y16, int64_t rows, int32_t cols, float scale,
+                                   void* stream) {
   MDEMI_REQUIRE(x && y && rows > 0 && cols > 0, "softmax_fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   if (cols <= 64 * SM_REG)
-    hipLaunchKernelGGL(softmax_wave_fwd, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, st, x, y, rows, cols, scale);
+    hipLaunchKernelGGL(softmax_wave_fwd, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, st, x, y, rows, cols, scale,
+                       (__bf16*)y16);
   else
-    hipLaunchKernelGGL(softmax_block_fwd, dim3((unsigned)rows), dim3(256), 0, st, x, y, cols, scale);
+    hipLaunchKernelGGL(softmax_block_fwd, dim3((unsigned)rows), dim3(256), 0, st, x, y, cols, scale, (__bf16*)y16);
   return check_launch("softmax_fwd");
 }
 
 extern "C" int mdemi_softmax_bwd(const float* y, const float* dy, float* dx, int64_t rows, int32_t cols, float scale,
                                  int32_t accumulate, void* stream) {
+  return mdemi_softmax_bwd16(y, dy, dx, nullptr, rows, cols, scale, accumulate, stream);
+}
+
+extern "C" int mdemi_softmax_bwd16(const float* y, const float* dy, float* dx, void* dx16, int64_t rows, int32_t cols,
+                                   float scale, int32_t accumulate, void* stream) {
   MDEMI_REQUIRE(y && dy && dx && rows > 0 && cols > 0, "softmax_bwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   if (cols <= 64 * SM_REG)
     hipLaunchKernelGGL(softmax_wave_bwd, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, st, y, dy, dx, rows, cols, scale,
-                       accumulate);
+                       accumulate, (__bf16*)dx16);
   else
-    hipLaunchKernelGGL(softmax_block_bwd, dim3((unsigned)rows), dim3(256), 0, st, y, dy, dx, cols, scale, accumulate);
+    hipLaunchKernelGGL(softmax_block_bwd, dim3((unsigned)rows), dim3(256), 0, st, y, dy, dx, cols, scale, accumulate,
+                       (__bf16*)dx16);
   return check_launch("softmax_bwd");
 }
 
@@ -626,12 +658,19 @@ extern "C" int mdemi_dropout(const float* x, float* y, int64_t n, float p, uint6
 
 extern "C" int mdemi_dropout_dev(const float* x, float* y, int64_t n, float p, const uint64_t* seed_dev,
                                  uint64_t seed_add, uint64_t offset, void* stream) {
+  return mdemi_dropout_dev16(x, y, nullptr, n, p, seed_dev, seed_add, offset, stream);
+}
+
+extern "C" int mdemi_dropout_dev16(const float* x, float* y, void* y16, int64_t n, float p, const uint64_t* seed_dev,
+                                   uint64_t seed_add, uint64_t offset, void* stream) {
   MDEMI_REQUIRE(x && y && n > 0 && p > 0.f && p < 1.f && seed_dev, "dropout_dev: bad args");
-  if (n % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+  const bool v4 = n % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)y16 & 7) == 0;
+  MDEMI_REQUIRE(!y16 || v4, "dropout_dev16: the bf16 copy needs n %% 4 == 0 and aligned buffers");
+  if (v4) {
     const int64_t n4 = n / 4;
     const unsigned g = (unsigned)std::min<int64_t>(cdiv(n4, 256), 8192);
     hipLaunchKernelGGL(dropout_dev4_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float4*)x, (float4*)y,
-                       n4, p, 1.f / (1.f - p), seed_dev, seed_add, offset);
+                       n4, p, 1.f / (1.f - p), seed_dev, seed_add, offset, (dp_bf16x4_t*)y16);
   } else {
     hipLaunchKernelGGL(dropout_dev_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, p,
                        1.f / (1.f - p), seed_dev, seed_add, offset);

@@ -10,11 +10,16 @@ namespace mdemi {
 
 constexpr int LN_THREADS = 256;
 
+typedef __bf16 ln_bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float ln_f32x4_t __attribute__((ext_vector_type(4)));
+
+// y16 (optional): the RNE bf16 copy of y, for a bf16 GEMM that reads the output (bf16 storage)
 template <int CACHE>
 __global__ __launch_bounds__(LN_THREADS) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                            const float* __restrict__ bta, float* __restrict__ y,
                                                            float* __restrict__ mean, float* __restrict__ rstd,
-                                                           int64_t rows, int C, float eps) {
+                                                           int64_t rows, int C, float eps,
+                                                           __bf16* __restrict__ y16) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * LN_THREADS + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * LN_THREADS) >> 6;
@@ -53,6 +58,10 @@ __global__ __launch_bounds__(LN_THREADS) void ln_fwd_kernel(const float* __restr
         o.z = (v[q].z - mu) * rs * gg.z + bb.z;
         o.w = (v[q].w - mu) * rs * gg.w + bb.w;
         yr[c4] = o;
+        if (y16) {
+          const ln_f32x4_t ov = {o.x, o.y, o.z, o.w};
+          *reinterpret_cast<ln_bf16x4_t*>(y16 + r * C + 4 * c4) = __builtin_convertvector(ov, ln_bf16x4_t);
+        }
       }
     }
     if (lane == 0) {
@@ -192,13 +201,19 @@ using namespace mdemi;
 extern "C" int mdemi_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y,
                                    float* mean, float* rstd, int64_t rows, int32_t C, float eps,
                                    void* stream) {
+  return mdemi_layernorm_fwd16(x, gamma, beta, y, nullptr, mean, rstd, rows, C, eps, stream);
+}
+
+extern "C" int mdemi_layernorm_fwd16(const float* x, const float* gamma, const float* beta, float* y, void* y16,
+                                     float* mean, float* rstd, int64_t rows, int32_t C, float eps, void* stream) {
   MDEMI_REQUIRE(x && gamma && beta && y && rows > 0 && C > 0, "layernorm_fwd: bad args");
+  MDEMI_REQUIRE(!y16 || ((uintptr_t)y16 & 7) == 0, "layernorm_fwd16: y16 must be 8-B aligned");
   MDEMI_REQUIRE(C % 4 == 0, "layernorm_fwd: C %% 4 != 0 (C=%d)", C);
   const int cache = ln_cache(C);
   MDEMI_REQUIRE(cache > 0, "layernorm_fwd: C=%d too large", C);
   hipStream_t st = (hipStream_t)stream;
   LN_DISPATCH(cache, ln_fwd_kernel, dim3(ln_fwd_blocks(rows)), dim3(LN_THREADS), 0, st, x, gamma, beta, y, mean,
-              rstd, rows, C, eps);
+              rstd, rows, C, eps, (__bf16*)y16);
   return check_launch("layernorm_fwd");
 }
 

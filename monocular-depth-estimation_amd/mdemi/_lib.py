@@ -138,6 +138,7 @@ _SIGS = {
     "mdemi_binhead_bwd_workspace_size": (sz, [i32, i32, i64]),
     "mdemi_binhead_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i64, i32, vp, vp]),
     "mdemi_layernorm_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
+    "mdemi_layernorm_fwd16": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
     "mdemi_layernorm_bwd_workspace_size": (sz, [i64, i32]),
     "mdemi_layernorm_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp, vp]),
     "mdemi_layernorm_bwd_add": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp, vp]),
@@ -189,9 +190,12 @@ _SIGS = {
     "mdemi_se_gate_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "mdemi_softmax_fwd": (ctypes.c_int, [vp, vp, i64, i32, f32, vp]),
     "mdemi_softmax_bwd": (ctypes.c_int, [vp, vp, vp, i64, i32, f32, i32, vp]),
+    "mdemi_softmax_fwd16": (ctypes.c_int, [vp, vp, vp, i64, i32, f32, vp]),
+    "mdemi_softmax_bwd16": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, f32, i32, vp]),
     "mdemi_act_fwd": (ctypes.c_int, [vp, vp, i64, i32, vp]),
     "mdemi_dropout": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "mdemi_dropout_dev": (ctypes.c_int, [vp, vp, i64, f32, vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
+    "mdemi_dropout_dev16": (ctypes.c_int, [vp, vp, vp, i64, f32, vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "mdemi_binhead_nhwc_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, vp]),
     "mdemi_binhead_nhwc_bwd_workspace_size": (sz, [i32, i64, i32]),
     "mdemi_binhead_nhwc_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, vp, vp]),

@@ -95,9 +95,11 @@ def _draw_seed(device):
     return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
 
 
-def _drop(src_ptr, dst_ptr, n, p, seed, add=0, offset=0):
-    """Inverted dropout of n floats; mask = hash(seed[0] + add, offset + i)."""
-    L.call("mdemi_dropout_dev", src_ptr, dst_ptr, n, float(p), seed.data_ptr(), add, offset, L.stream())
+def _drop(src_ptr, dst_ptr, n, p, seed, add=0, offset=0, dst16_ptr=None):
+    """Inverted dropout of n floats; mask = hash(seed[0] + add, offset + i); dst16_ptr: also
+    the bf16 copy of the result."""
+    L.call("mdemi_dropout_dev16", src_ptr, dst_ptr, dst16_ptr, n, float(p), seed.data_ptr(), add, offset,
+           L.stream())
 
 
 # Matmul precision of every libmdemi GEMM:
@@ -198,6 +200,18 @@ def new_b16_like(t):
     if _PRECISION[0] != "bf16" or not _B16_STORAGE[0]:
         return None
     return torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
+
+
+# autograd nodes whose backward runs bf16 GEMMs on the gradient of their output
+_GEMM_BWD_NODES = frozenset(("_LinearFnBackward", "_Conv2dFnBackward", "_MlpFnBackward", "_LinearActFnBackward",
+                             "_AttentionFnBackward", "_BatchedGemmFnBackward"))
+
+
+def grad_feeds_gemm(x):
+    """True (bf16 storage on) when x came from an op whose backward reads x's gradient as a
+    bf16 GEMM operand: the op producing that gradient then writes its bf16 copy too."""
+    return (_PRECISION[0] == "bf16" and _B16_STORAGE[0] and x.grad_fn is not None
+            and type(x.grad_fn).__name__ in _GEMM_BWD_NODES)
 
 
 class matmul_precision:
@@ -366,6 +380,7 @@ class _LinearFn(torch.autograd.Function):
         res2 = _c(residual).reshape(x2.shape[0], -1) if residual is not None else None
         out = linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2, drop_scale=drop_scale)
         ctx.save_for_backward(x2, weight)
+        ctx.dx16 = grad_feeds_gemm(x)
         ctx.drop_scale = drop_scale
         ctx.in_gelu = in_gelu
         ctx.has_bias = bias is not None
@@ -384,10 +399,13 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, device=dy.device, dtype=torch.float32)
+            dx16 = new_b16_like(dx) if ctx.dx16 else None  # dX is the next GEMM backward's operand
             # dX[M,K] = dY[M,N] . W[N,K]  (times gelu'(h) when the forward read gelu(h))
             gemm(dy2, weight, dx, M, K, N, lda=N, ldb=K, ldc=K, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
                  act=L.ACT_GELU_GRAD if ctx.in_gelu else L.ACT_NONE, aux=x2 if ctx.in_gelu else None,
-                 ldaux=K)
+                 ldaux=K, c16=dx16)
+            if dx16 is not None:
+                set_b16(dx, dx16)
             dx = dx.view(ctx.xshape)
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         if want_db:
@@ -432,11 +450,14 @@ class _MlpFn(torch.autograd.Function):
         Hd, N = w1.shape[0], w2.shape[0]
         h = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
         g = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
+        g16 = new_b16_like(g) if g.numel() % 4 == 0 else None  # fc2's operand (bf16 storage)
         gemm(x2, _c(w1), g, M, Hd, K, lda=K, ldb=K, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
              bias=b1, bias_mode=L.BIAS_COL if b1 is not None else L.BIAS_NONE, act=act,
-             preact=h, ldpre=Hd, split_k=1)
+             preact=h, ldpre=Hd, split_k=1, c16=g16 if p_mid == 0.0 else None)
         if p_mid > 0.0:
-            _drop(g.data_ptr(), g.data_ptr(), g.numel(), p_mid, seed)
+            _drop(g.data_ptr(), g.data_ptr(), g.numel(), p_mid, seed, dst16_ptr=L.ptr(g16))
+        if g16 is not None:
+            set_b16(g, g16)
         res2 = _c(residual).reshape(M, N) if residual is not None else None
         if p_out > 0.0:
             out = linear_fwd_raw(g, _c(w2), b2)
@@ -465,7 +486,10 @@ class _MlpFn(torch.autograd.Function):
         dev = dy.device
         if p_out > 0.0:
             d2 = torch.empty_like(dy2)
-            _drop(dy2.data_ptr(), d2.data_ptr(), d2.numel(), p_out, seed, add=1)
+            d216 = new_b16_like(d2) if d2.numel() % 4 == 0 and dy2.data_ptr() % 16 == 0 else None
+            _drop(dy2.data_ptr(), d2.data_ptr(), d2.numel(), p_out, seed, add=1, dst16_ptr=L.ptr(d216))
+            if d216 is not None:
+                set_b16(d2, d216)  # the operand of both fc2 gradient GEMMs
         else:
             d2 = dy2
         dw2 = torch.empty(N, Hd, device=dev, dtype=torch.float32)
@@ -479,8 +503,11 @@ class _MlpFn(torch.autograd.Function):
             L.call("mdemi_elementwise", L.EW_ACT_BWD, h.data_ptr(), dh.data_ptr(), dh.data_ptr(), dh.numel(),
                    float(act), 0.0, L.stream())
         else:
+            dh16 = new_b16_like(dh)  # the operand of both fc1 gradient GEMMs
             gemm(d2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
-                 act=L.ACT_GRAD_OF[act], aux=h, ldaux=Hd)
+                 act=L.ACT_GRAD_OF[act], aux=h, ldaux=Hd, c16=dh16)
+            if dh16 is not None:
+                set_b16(dh, dh16)
         del h, g
         dw1 = torch.empty(Hd, K, device=dev, dtype=torch.float32)
         db1 = torch.empty(Hd, device=dev, dtype=torch.float32) if has_b1 else None
@@ -706,16 +733,20 @@ def patch_embed(img_nchw, weight, bias):
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
+    def forward(ctx, x, weight, bias, eps, out_b16=False):
+        """out_b16: y feeds a bf16 GEMM -- write its bf16 copy in the same sweep (bf16 storage)."""
         _require_cuda(x, weight, bias)
         x = _c(x)
         C = x.shape[-1]
         rows = x.numel() // C
         y = torch.empty_like(x)
+        y16 = new_b16_like(y) if out_b16 else None
         mean = torch.empty(rows, device=x.device, dtype=torch.float32)
         rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
-        L.call("mdemi_layernorm_fwd", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
+        L.call("mdemi_layernorm_fwd16", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(), L.ptr(y16),
                mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), L.stream())
+        if y16 is not None:
+            set_b16(y, y16)
         ctx.save_for_backward(x, weight, mean, rstd)
         return y
 
@@ -733,7 +764,7 @@ class _LayerNormFn(torch.autograd.Function):
         L.check(lib.mdemi_layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                         weight.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), rows, C, 0,
                                         ws.data_ptr(), L.stream()), "layernorm_bwd")
-        return dx, dg, db, None
+        return dx, dg, db, None, None
 
 
 class _LayerNormSkipFn(torch.autograd.Function):
@@ -787,8 +818,9 @@ def layer_norm_skip(x, weight, bias, eps=1e-5):
     return _LayerNormSkipFn.apply(x, weight, bias, eps)
 
 
-def layer_norm(x, weight, bias, eps=1e-5):
-    return _LayerNormFn.apply(x, weight, bias, eps)
+def layer_norm(x, weight, bias, eps=1e-5, out_b16=False):
+    """out_b16: the output feeds a bf16 GEMM (bf16 storage writes its bf16 copy too)."""
+    return _LayerNormFn.apply(x, weight, bias, eps, out_b16)
 
 
 # --------------------------------------------------------------------------
@@ -1125,8 +1157,7 @@ class _ChNormFn(torch.autograd.Function):
         hw = x[0].numel() // c
         y = torch.empty_like(x)
         y16 = new_b16_like(y) if (out_b16 and running is not None and is_bn) else None
-        ctx.dx16 = bool(is_bn and _PRECISION[0] == "bf16" and _B16_STORAGE[0] and x.grad_fn is not None
-                        and type(x.grad_fn).__name__ == "_Conv2dFnBackward")
+        ctx.dx16 = bool(is_bn and grad_feeds_gemm(x))
         nstat = c if is_bn else n * groups
         mean = torch.empty(nstat, device=x.device, dtype=torch.float32)
         rstd = torch.empty(nstat, device=x.device, dtype=torch.float32)
@@ -1606,6 +1637,7 @@ class _DropoutFn(torch.autograd.Function):
         y = torch.empty_like(x)
         _drop(x.data_ptr(), y.data_ptr(), x.numel(), p, seed, offset=offset)
         ctx.cfg = (p, seed, offset)
+        ctx.dx16 = grad_feeds_gemm(x) and x.numel() % 4 == 0
         return y
 
     @staticmethod
@@ -1613,7 +1645,10 @@ class _DropoutFn(torch.autograd.Function):
         p, seed, offset = ctx.cfg
         dy = _c(dy)
         dx = torch.empty_like(dy)
-        _drop(dy.data_ptr(), dx.data_ptr(), dy.numel(), p, seed, offset=offset)
+        dx16 = new_b16_like(dx) if ctx.dx16 and dy.data_ptr() % 16 == 0 else None
+        _drop(dy.data_ptr(), dx.data_ptr(), dy.numel(), p, seed, offset=offset, dst16_ptr=L.ptr(dx16))
+        if dx16 is not None:
+            set_b16(dx, dx16)
         return dx, None, None, None
 
 
@@ -1824,7 +1859,7 @@ class _AttentionFn(torch.autograd.Function):
     attentions (luna_layer.py:202-250) and SelfAttentionBlock (self_attention.py:61-80)."""
 
     @staticmethod
-    def forward(ctx, qsrc, ksrc, vsrc, cfg):
+    def forward(ctx, qsrc, ksrc, vsrc, cfg, out_b16=False):
         B, Sq, Sk, heads, dqk, dv, q_off, k_off, v_off, scale, p, seed = cfg
         _require_cuda(qsrc, ksrc, vsrc)
         ldq, ldk, ldv = qsrc.shape[-1], ksrc.shape[-1], vsrc.shape[-1]
@@ -1834,17 +1869,27 @@ class _AttentionFn(torch.autograd.Function):
         gemm(qsrc, ksrc, P, Sq, Sk, dqk, lda=ldq, ldb=ldk, ldc=Sk, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
              batch=B * heads, a_bstride=Sq * ldq, b_bstride=Sk * ldk, c_bstride=heads * hs, a_off=q_off,
              b_off=k_off, inner=(heads, dqk, dqk, hs))
-        L.call("mdemi_softmax_fwd", P.data_ptr(), P.data_ptr(), B * heads * Sq, Sk, float(scale), L.stream())
+        # bf16 storage: the probabilities' bf16 copy (P.V's operand) from the softmax sweep, or the
+        # dropped-out ones' from the dropout sweep
+        P16 = new_b16_like(P) if (p == 0.0 or P.numel() % 4 == 0) else None
+        L.call("mdemi_softmax_fwd16", P.data_ptr(), P.data_ptr(), L.ptr(P16) if p == 0.0 else None,
+               B * heads * Sq, Sk, float(scale), L.stream())
         Pd = P
         if p > 0.0:
             Pd = torch.empty_like(P)
-            _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed)
+            _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed, dst16_ptr=L.ptr(P16))
+        if P16 is not None:
+            set_b16(Pd, P16)
         out = torch.empty(B * Sq, heads * dv, device=dev, dtype=torch.float32)
+        out16 = new_b16_like(out) if out_b16 else None  # the output projection's operand
         gemm(Pd, vsrc, out, Sq, dv, Sk, lda=Sk, ldb=ldv, ldc=heads * dv, a_layout=L.L_KCONTIG,
              b_layout=L.L_MNCONTIG, batch=B * heads, a_bstride=heads * hs, b_bstride=Sk * ldv,
-             c_bstride=Sq * heads * dv, b_off=v_off, inner=(heads, hs, dv, dv))
+             c_bstride=Sq * heads * dv, b_off=v_off, inner=(heads, hs, dv, dv), c16=out16)
+        if out16 is not None:
+            set_b16(out, out16)
         ctx.save_for_backward(qsrc, ksrc, vsrc, P)
         ctx.cfg = cfg
+        ctx.grad16 = tuple(grad_feeds_gemm(t) for t in (qsrc, ksrc, vsrc))
         ctx.set_materialize_grads(False)  # unused probabilities: no zero fill + add of [B,h,Sq,Sk]
         return out, P
 
@@ -1859,16 +1904,22 @@ class _AttentionFn(torch.autograd.Function):
             Pd = torch.empty_like(P)
             _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed)
         # one gradient buffer per distinct source tensor; columns outside the used slices are zero
-        bufs, spans = {}, {}
+        bufs, spans, b16s = {}, {}, {}
         for t, off, width in ((qsrc, q_off, heads * dqk), (ksrc, k_off, heads * dqk), (vsrc, v_off, heads * dv)):
             spans.setdefault(id(t), []).append((off, width))
+        want16 = {}
+        for t, w in zip((qsrc, ksrc, vsrc), ctx.grad16):
+            want16[id(t)] = want16.get(id(t), False) or w
         for t in (qsrc, ksrc, vsrc):
             if id(t) in bufs:
                 continue
             covered = sum(w for _, w in spans[id(t)])
             full = covered == t.shape[-1] and dout is not None
             bufs[id(t)] = torch.empty_like(t) if full else torch.zeros_like(t)
+            # a fully written gradient that a GEMM backward reads next: its bf16 copy too
+            b16s[id(t)] = new_b16_like(t) if full and want16[id(t)] else None
         dq, dk, dvv = bufs[id(qsrc)], bufs[id(ksrc)], bufs[id(vsrc)]
+        dq16, dk16, dv16 = b16s[id(qsrc)], b16s[id(ksrc)], b16s[id(vsrc)]
         dP = torch.empty_like(P)
         if dout is not None:
             dout = _c(dout)
@@ -1877,7 +1928,7 @@ class _AttentionFn(torch.autograd.Function):
                  c_bstride=heads * hs, b_off=v_off, inner=(heads, dv, dv, hs))
             gemm(Pd, dout, dvv, Sk, dv, Sq, lda=Sk, ldb=heads * dv, ldc=ldv, a_layout=L.L_MNCONTIG,
                  b_layout=L.L_MNCONTIG, batch=B * heads, a_bstride=heads * hs, b_bstride=Sq * heads * dv,
-                 c_bstride=Sk * ldv, c_off=v_off, inner=(heads, hs, dv, dv))
+                 c_bstride=Sk * ldv, c_off=v_off, inner=(heads, hs, dv, dv), c16=dv16)
             if p > 0.0:
                 _drop(dP.data_ptr(), dP.data_ptr(), dP.numel(), p, seed)
             if dP_ext is not None:
@@ -1888,30 +1939,37 @@ class _AttentionFn(torch.autograd.Function):
             _copy2d(_c(dP_ext).view(-1, Sk), dP.view(-1, Sk))
         else:
             dP.zero_()
-        L.call("mdemi_softmax_bwd", P.data_ptr(), dP.data_ptr(), dP.data_ptr(), B * heads * Sq, Sk, float(scale), 0,
-               L.stream())
+        dP16 = new_b16_like(dP)  # dS: the operand of the dQ and dK GEMMs
+        L.call("mdemi_softmax_bwd16", P.data_ptr(), dP.data_ptr(), dP.data_ptr(), L.ptr(dP16), B * heads * Sq, Sk,
+               float(scale), 0, L.stream())
+        if dP16 is not None:
+            set_b16(dP, dP16)
         gemm(dP, ksrc, dq, Sq, dqk, Sk, lda=Sk, ldb=ldk, ldc=ldq, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
              batch=B * heads, a_bstride=heads * hs, b_bstride=Sk * ldk, c_bstride=Sq * ldq, b_off=k_off,
-             c_off=q_off, inner=(heads, hs, dqk, dqk))
+             c_off=q_off, inner=(heads, hs, dqk, dqk), c16=dq16)
         gemm(dP, qsrc, dk, Sk, dqk, Sq, lda=Sk, ldb=ldq, ldc=ldk, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
              batch=B * heads, a_bstride=heads * hs, b_bstride=Sq * ldq, c_bstride=Sk * ldk, b_off=q_off,
-             c_off=k_off, inner=(heads, hs, dqk, dqk))
+             c_off=k_off, inner=(heads, hs, dqk, dqk), c16=dk16)
+        for t in (qsrc, ksrc, vsrc):
+            if b16s[id(t)] is not None:
+                set_b16(bufs[id(t)], b16s[id(t)])
         seen, grads = set(), []
         for t, g in ((qsrc, dq), (ksrc, dk), (vsrc, dvv)):
             grads.append(None if id(t) in seen else g)
             seen.add(id(t))
-        return grads[0], grads[1], grads[2], None
+        return grads[0], grads[1], grads[2], None, None
 
 
 def attention(qsrc, ksrc, vsrc, B, Sq, Sk, heads, dqk, dv, scale, q_off=0, k_off=0, v_off=0, p=0.0,
-              training=False):
+              training=False, out_b16=False):
     """Returns (out [B*Sq, heads*dv], probs [B, heads, Sq, Sk]).  q/k/v are column slices
     (offsets q_off/k_off/v_off, head-major) of 2-D token-major buffers [B*S, ld]; a buffer may
-    feed several of them (e.g. a fused qkv projection)."""
+    feed several of them (e.g. a fused qkv projection).  out_b16: `out` feeds a bf16 GEMM
+    (the output projection) -- write its bf16 copy too (bf16 storage)."""
     p = float(p) if training else 0.0
     seed = _draw_seed(qsrc.device) if p > 0.0 else None
     cfg = (B, Sq, Sk, heads, dqk, dv, q_off, k_off, v_off, float(scale), p, seed)
-    return _AttentionFn.apply(_c(qsrc), _c(ksrc), _c(vsrc), cfg)
+    return _AttentionFn.apply(_c(qsrc), _c(ksrc), _c(vsrc), cfg, out_b16)
 
 
 def _bgemm_raw(A, B, ta, tb, bias=None):

@@ -46,23 +46,24 @@ class PreNormLunaBlock(nn.Module):
         """hidden (B*HW, d), aux (B*K, a) -> (hidden', aux', attn1 (B,nh,K,HW), attn2 (B,nh,HW,K))."""
         d, nh, qk = self.hidden_dim, self.num_heads, self.qk_proj_dim
         tr = self.training
-        aux_n = mf.layer_norm(aux, self.aux_norm.weight, self.aux_norm.bias, self.aux_norm.eps)
-        hidden_n = mf.layer_norm(hidden, self.norm.weight, self.norm.bias, self.norm.eps)
+        aux_n = mf.layer_norm(aux, self.aux_norm.weight, self.aux_norm.bias, self.aux_norm.eps, out_b16=True)
+        hidden_n = mf.layer_norm(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
         q1 = mf.linear(aux_n, self.q1_proj.weight, self.q1_proj.bias)                       # (B*K, qk)
         w_h = torch.cat([self.k1_proj.weight, self.v1_proj.weight, self.q2_proj.weight])
         b_h = torch.cat([self.k1_proj.bias, self.v1_proj.bias, self.q2_proj.bias])
         kvq = mf.linear(hidden_n, w_h, b_h)                                                  # (B*HW, qk+d+qk)
         out1, attn1 = mf.attention(q1, kvq, kvq, B, K, HW, nh, qk // nh, d // nh, self.attn_scale, q_off=0,
-                                   k_off=0, v_off=qk, p=self.attn_drop.p, training=tr)
+                                   k_off=0, v_off=qk, p=self.attn_drop.p, training=tr, out_b16=True)
         out1 = mf.linear(out1, self.o1_proj.weight, self.o1_proj.bias)                      # (B*K, a)
         out1 = mf.dropout(out1, self.drop.p, tr)
         aux_out = mf.add(aux, out1)
-        out_n = mf.layer_norm(out1, self.inter_norm.weight, self.inter_norm.bias, self.inter_norm.eps)
+        out_n = mf.layer_norm(out1, self.inter_norm.weight, self.inter_norm.bias, self.inter_norm.eps,
+                                  out_b16=True)
         w_a = torch.cat([self.k2_proj.weight, self.v2_proj.weight])
         b_a = torch.cat([self.k2_proj.bias, self.v2_proj.bias])
         kv2 = mf.linear(out_n, w_a, b_a)                                                     # (B*K, qk+d)
         out2, attn2 = mf.attention(kvq, kv2, kv2, B, HW, K, nh, qk // nh, d // nh, self.attn_scale,
-                                   q_off=qk + d, k_off=0, v_off=qk, p=self.attn_drop.p, training=tr)
+                                   q_off=qk + d, k_off=0, v_off=qk, p=self.attn_drop.p, training=tr, out_b16=True)
         if tr and self.drop.p > 0.0:
             out2 = mf.dropout(mf.linear(out2, self.o2_proj.weight, self.o2_proj.bias), self.drop.p, True)
             out = mf.add(hidden, out2)

@@ -31,12 +31,12 @@ class SelfAttentionBlock(nn.Module):
     def forward(self, hidden, B, S):
         """hidden (B*S, d) -> (hidden', attn (B, nh, S, S))."""
         kq, d, nh = self.key_query_dim, self.hidden_dim, self.num_heads
-        h = mf.layer_norm(hidden, self.norm.weight, self.norm.bias, self.norm.eps)
+        h = mf.layer_norm(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
         w = torch.cat([self.query_proj.weight, self.key_proj.weight, self.value_proj.weight])
         b = torch.cat([self.query_proj.bias, self.key_proj.bias, self.value_proj.bias])
         qkv = mf.linear(h, w, b)
         o, attn = mf.attention(qkv, qkv, qkv, B, S, S, nh, kq // nh, d // nh, self.attn_scale, q_off=0, k_off=kq,
-                               v_off=2 * kq, p=self.attn_drop.p, training=self.training)
+                               v_off=2 * kq, p=self.attn_drop.p, training=self.training, out_b16=True)
         if self.training and self.drop.p > 0.0:
             out = mf.add(mf.dropout(mf.linear(o, self.out_proj.weight, self.out_proj.bias), self.drop.p, True),
                          hidden)

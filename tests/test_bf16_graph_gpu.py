@@ -362,7 +362,7 @@ def test_every_bf16_gemm_of_the_configs4_step_is_exact(mf):
         a_op, b_op = kw.get("a_op", 0), kw.get("b_op", 0)
         Ar = (torch.nn.functional.gelu(A) if a_op else A).to(torch.bfloat16).float()
         Br = (torch.nn.functional.gelu(B) if b_op else B).to(torch.bfloat16).float()
-        kw_ref = dict(kw, a_op=L.OP_NONE, b_op=L.OP_NONE, rowsum_a=None)
+        kw_ref = dict(kw, a_op=L.OP_NONE, b_op=L.OP_NONE, rowsum_a=None, a16=None, b16=None, c16=None)
         C.copy_(before)
         for k, v in saved.items():
             kw[k].copy_(v)
@@ -378,6 +378,9 @@ def test_every_bf16_gemm_of_the_configs4_step_is_exact(mf):
         for k, v in after.items():
             kw[k].copy_(v)
         torch.cuda.synchronize()
+        if kw.get("c16") is not None and kw.get("c_off", 0) == 0 and kw.get("batch", 1) == 1 and \
+                kw["ldc"] == N and C.numel() == M * N:  # the bf16 copy it wrote is the RNE of its result
+            assert torch.equal(kw["c16"], got.to(torch.bfloat16)), ("c16", M, N, K)
         err = (got - ref).abs().max().item()
         lim = (2.0 ** -8 if (a_op or b_op) else 2.0 * ACC_RTOL) * absprod + 1e-30
         stats["calls"] += 1
