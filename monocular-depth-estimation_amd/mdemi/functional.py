@@ -58,6 +58,8 @@ def _split_for(M, N, K):
     # k-tile several times faster, so there the slab combine dominates and the round-4 rule
     # measured better (Depthformer bf16 140.3 vs 138.2 img/s, profiles/round5/ab_split_policy.txt)
     if tiles >= 32 and not bf16 and _SPLIT_POLICY == "fill":
+        if 384 <= tiles <= 512:  # one round at two workgroups per CU already: a split only adds slabs
+            return 1            # (9600x768x3072: split 5 measured 112 vs 118 TF/s unsplit)
         return _split_fill(tiles, min(ktiles // min_kt, 128), 1 if tiles >= 384 else min(
             max(1, _target_blocks() // tiles), ktiles // min_kt, 128))
     if tiles >= 384:
