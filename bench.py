@@ -331,9 +331,10 @@ class _HbmTimers:
         dpred and writes dlogits, 4*B*HW*(2K+4) B;
       winattn_fwd/bwd (fused shifted-window attention): fwd reads q, k, v and
         writes out, 16*C B per token; bwd reads q, k, v, out, dout and writes dq, dk, dv,
-        32*C B per token (the window's MFMA work rides on the same pass).  The entry also
-        launches the small relative-position-bias expansion (and, backward, its gradient
-        scatter): a few us each, counted in the window."""
+        32*C B per token (the window's MFMA work rides on the same pass).  The forward entry
+        also launches the small relative-position-bias expansion, which the backward reuses;
+        the backward adds the bias gradient's column sum and scatter: a few us each, counted in
+        the window."""
 
     def __init__(self, lib):
         def wa_bytes(per_token):
@@ -345,7 +346,7 @@ class _HbmTimers:
         self.specs = {"mdemi_binhead_nhwc_fwd": ("binhead_nhwc_fwd", lambda a: 4.0 * a[4] * a[5] * (a[6] + 3)),
                       "mdemi_binhead_nhwc_bwd": ("binhead_nhwc_bwd", lambda a: 4.0 * a[7] * a[8] * (2 * a[9] + 4)),
                       "mdemi_winattn_fwd": ("winattn_fwd", wa_bytes(16.0)),
-                      "mdemi_winattn_bwd": ("winattn_bwd", wa_bytes(32.0))}
+                      "mdemi_winattn_bwd_bias": ("winattn_bwd", wa_bytes(32.0))}
         self.lib = lib
         self.orig = {entry: getattr(lib, entry) for entry in self.specs}
         self.recs = {name: [] for name, _ in self.specs.values()}

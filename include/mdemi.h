@@ -279,6 +279,11 @@ size_t mdemi_winattn_fwd_workspace_size(const mdemi_winattn_desc* d);
 int mdemi_winattn_fwd(const mdemi_winattn_desc* d, void* stream);
 size_t mdemi_winattn_bwd_workspace_size(const mdemi_winattn_desc* d);
 int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream);
+/* The same backward reusing the forward's expanded relative-position bias: bias_expanded =
+ * the first mdemi_winattn_fwd_workspace_size() bytes of the forward call's workspace, kept
+ * unchanged since (the table it expands is the same parameter); null = expand it again.
+ * One launch fewer per backward (WindowAttention.forward, swin_transformer.py:112-144). */
+int mdemi_winattn_bwd_bias(const mdemi_winattn_desc* d, const float* bias_expanded, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Scale-invariant log loss (restated; the reference's loss module is        */

@@ -755,6 +755,10 @@ extern "C" size_t mdemi_winattn_bwd_workspace_size(const mdemi_winattn_desc* d) 
 }
 
 extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
+  return mdemi_winattn_bwd_bias(d, nullptr, stream);
+}
+
+extern "C" int mdemi_winattn_bwd_bias(const mdemi_winattn_desc* d, const float* bias_expanded, void* stream) {
   WinParams p;
   int nwin;
   int rc = make_params(d, p, nwin);
@@ -775,8 +779,11 @@ extern "C" int mdemi_winattn_bwd(const mdemi_winattn_desc* d, void* stream) {
   float* biasT = (float*)(ws + wa_part_bytes(items, R));
   float* sums = (float*)((char*)biasT + wa_bias_bytes(d));
   void* cws = (char*)sums + align_up((size_t)d->heads * R * 4, 256);
-  hipLaunchKernelGGL(wa_bias_kernel, dim3(d->heads * 16), dim3(256), 0, st, d->rpb_table, d->heads, biasT,
-                     (float*)nullptr);
+  if (bias_expanded)  // the forward's expansion of the same table (mdemi_winattn_fwd's workspace)
+    biasT = const_cast<float*>(bias_expanded);
+  else
+    hipLaunchKernelGGL(wa_bias_kernel, dim3(d->heads * 16), dim3(256), 0, st, d->rpb_table, d->heads, biasT,
+                       (float*)nullptr);
   hipLaunchKernelGGL((winattn_bwd_kernel<7, 32>), dim3((unsigned)cdiv(items, WA_WAVES)), dim3(64 * WA_WAVES), 0, st,
                      p, (const float*)biasT, items);
   int rc2 = colsum_launch(p.partial, nwin, (int64_t)d->heads * R, (int64_t)d->heads * R, sums, 0, cws, st);

@@ -146,6 +146,7 @@ _SIGS = {
     "mdemi_winattn_fwd": (ctypes.c_int, [ctypes.POINTER(WinAttnDesc), vp]),
     "mdemi_winattn_bwd_workspace_size": (sz, [ctypes.POINTER(WinAttnDesc)]),
     "mdemi_winattn_bwd": (ctypes.c_int, [ctypes.POINTER(WinAttnDesc), vp]),
+    "mdemi_winattn_bwd_bias": (ctypes.c_int, [ctypes.POINTER(WinAttnDesc), vp, vp]),
     "mdemi_silog_workspace_size": (sz, [i32, i64]),
     "mdemi_silog_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, f32, f32, f32, i32, i32, vp, vp]),
     "mdemi_silog_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i64, f32, f32, f32, i32, i32, vp]),

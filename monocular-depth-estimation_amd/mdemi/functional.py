@@ -855,9 +855,14 @@ class _WindowAttnFn(torch.autograd.Function):
         lse = torch.empty(nwin, heads, ws * ws, device=qk.device, dtype=torch.float32)
         d.lse = lse.data_ptr()
         lib = L.load()
-        ws_f = L.workspace(lib.mdemi_winattn_fwd_workspace_size(ctypes.byref(d)), qk.device)
-        d.workspace, d.workspace_bytes = ws_f.data_ptr(), ws_f.numel()
+        # the forward's workspace is the expanded relative-position bias: a buffer of this call's
+        # own (heads x 16 KiB), kept for the backward instead of expanding the table again
+        bias_x = torch.empty(lib.mdemi_winattn_fwd_workspace_size(ctypes.byref(d)) // 4, device=qk.device,
+                             dtype=torch.float32)
+        d.workspace, d.workspace_bytes = bias_x.data_ptr(), 4 * bias_x.numel()
         L.check(lib.mdemi_winattn_fwd(ctypes.byref(d), L.stream()), "winattn_fwd")
+        ctx.bias_x = bias_x
+        ctx.rpb_version = rpb._version
         ctx.save_for_backward(qk, qk_bias, v, v_bias, rpb, out, lse)
         ctx.geom = geom
         ctx.has_qkb = qk_bias is not None
@@ -911,7 +916,9 @@ class _WindowAttnFn(torch.autograd.Function):
         need = lib.mdemi_winattn_bwd_workspace_size(ctypes.byref(d))
         ws = L.workspace(need, qk.device)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
-        L.check(lib.mdemi_winattn_bwd(ctypes.byref(d), L.stream()), "winattn_bwd")
+        # the forward's expansion is valid while the table is unchanged (no in-place update since)
+        bias_x = ctx.bias_x if rpb._version == ctx.rpb_version else None
+        L.check(lib.mdemi_winattn_bwd_bias(ctypes.byref(d), L.ptr(bias_x), L.stream()), "winattn_bwd")
         if ctx.has_qkb and dqk_bias is None:
             dqk_bias = torch.zeros_like(qk_bias)
             dqk_bias[:C] = pad_g[0]
