@@ -66,9 +66,10 @@ __global__ void colsum_final(const float* __restrict__ part, int nblk, int64_t c
 }
 
 // Short reductions (rows <= COLSUM_ONEPASS): one launch, no workspace.  A block
-// covers 32 columns with 32 row groups; each thread keeps 8 loads in flight
-// (rows ty, ty+32, ... in order), then the 32 group sums are added in group
-// order -- a fixed association, so the result is deterministic.
+// covers 32 columns with 32 row groups; each thread issues all its (<= 32) loads at
+// once -- one memory round trip instead of four -- and adds them in row order (rows
+// ty, ty+32, ...), then the 32 group sums are added in group order: a fixed
+// association, so the result is deterministic.
 constexpr int COLSUM_ONEPASS = 1024;
 __global__ __launch_bounds__(1024) void colsum_onepass(const float* __restrict__ x, int64_t rows, int64_t cols,
                                                        int64_t ld, float* __restrict__ out, float* __restrict__ out2,
@@ -78,16 +79,15 @@ __global__ __launch_bounds__(1024) void colsum_onepass(const float* __restrict__
   const int64_t c = (int64_t)blockIdx.x * 32 + tx;
   float s = 0.f;
   if (c < cols) {
-    for (int64_t r0 = ty; r0 < rows; r0 += 256) {
-      float v[8];
+    constexpr int NL = COLSUM_ONEPASS / 32;
+    float v[NL];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int64_t r = r0 + 32 * j;
-        v[j] = r < rows ? x[r * ld + c] : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j];
+    for (int j = 0; j < NL; ++j) {
+      const int64_t r = ty + 32 * j;
+      v[j] = r < rows ? x[r * ld + c] : 0.f;
     }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) s += v[j];
   }
   red[ty][tx] = s;
   __syncthreads();
