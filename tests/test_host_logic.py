@@ -58,3 +58,25 @@ def test_split_k_plan():
     for M, N, K in ((768, 768, 9600), (64, 792, 614400), (2304, 768, 9600)):
         s = mf._split_for(M, N, K)
         assert 1 <= s <= 512 and K / s >= 512 - 16
+
+
+def test_split_k_wave_quantisation_fp32():
+    """fp32 split factors by wave quantisation (functional._split_fill, round 5;
+    profiles/round5/split_study.txt): tiles x split workgroups fill whole rounds of one per CU,
+    384-512 tiles stay unsplit, narrow outputs keep their deep splits, bf16 keeps the round-4
+    rule."""
+    from mdemi import functional as mf
+    assert mf._split_for(768, 768, 9600) == 7        # 36 tiles x 7 = 252 workgroups (was 18: 648)
+    assert mf._split_for(384, 1536, 38400) == 7      # 36 tiles (was 28)
+    assert mf._split_for(2304, 768, 9600) == 7       # 108 tiles x 7 = 756 = 3 full rounds
+    assert mf._split_for(9600, 768, 3072) == 1       # 450 tiles: one round at two workgroups per CU
+    assert 2 <= mf._split_for(6144, 1536, 2400) <= 4  # 576 tiles: 2.25 rounds unsplit
+    assert mf._split_for(576, 192, 153600) == 102    # 10 tiles: the deep split stays
+    prev = mf._SPLIT_POLICY
+    try:
+        mf._SPLIT_POLICY = "legacy"
+        assert mf._split_for(768, 768, 9600) == 18
+    finally:
+        mf._SPLIT_POLICY = prev
+    with mf.matmul_precision("bf16"):
+        assert mf._split_for(768, 768, 9600) == 28   # the round-4 rule: 1024 // 36
