@@ -775,16 +775,19 @@ class _LayerNormSkipFn(torch.autograd.Function):
     (mdemi_layernorm_bwd_add) instead of an extra elementwise add of autograd."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
+    def forward(ctx, x, weight, bias, eps, out_b16=False):
         _require_cuda(x, weight, bias)
         x = _c(x)
         C = x.shape[-1]
         rows = x.numel() // C
         y = torch.empty_like(x)
+        y16 = new_b16_like(y) if out_b16 else None  # LN(x) feeds a bf16 GEMM (bf16 storage)
         mean = torch.empty(rows, device=x.device, dtype=torch.float32)
         rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
-        L.call("mdemi_layernorm_fwd", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
+        L.call("mdemi_layernorm_fwd16", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(), L.ptr(y16),
                mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), L.stream())
+        if y16 is not None:
+            set_b16(y, y16)
         ctx.save_for_backward(x, weight, mean, rstd)
         ctx.set_materialize_grads(False)  # an unused output's gradient stays None (no zero fill)
         skip = x.view_as(x)
@@ -801,7 +804,7 @@ class _LayerNormSkipFn(torch.autograd.Function):
         lib = L.load()
         ws = L.workspace(lib.mdemi_layernorm_bwd_workspace_size(rows, C), x.device)
         if dy is None:
-            return dskip, None, None, None
+            return dskip, None, None, None, None
         dy = _c(dy)
         if dskip is None:
             L.check(lib.mdemi_layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
@@ -812,12 +815,13 @@ class _LayerNormSkipFn(torch.autograd.Function):
             L.check(lib.mdemi_layernorm_bwd_add(dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                                 weight.data_ptr(), dskip.data_ptr(), dx.data_ptr(), dg.data_ptr(),
                                                 db.data_ptr(), rows, C, ws.data_ptr(), L.stream()), "layernorm_bwd_add")
-        return dx, dg, db, None
+        return dx, dg, db, None, None
 
 
-def layer_norm_skip(x, weight, bias, eps=1e-5):
-    """(LayerNorm(x), x) for a residual block; use the second output as the residual."""
-    return _LayerNormSkipFn.apply(x, weight, bias, eps)
+def layer_norm_skip(x, weight, bias, eps=1e-5, out_b16=False):
+    """(LayerNorm(x), x) for a residual block; use the second output as the residual.
+    out_b16: LayerNorm(x) feeds a bf16 GEMM (bf16 storage writes its bf16 copy too)."""
+    return _LayerNormSkipFn.apply(x, weight, bias, eps, out_b16)
 
 
 def layer_norm(x, weight, bias, eps=1e-5, out_b16=False):

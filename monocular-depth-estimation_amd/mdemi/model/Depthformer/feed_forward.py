@@ -28,6 +28,7 @@ class FeedForwardBlock(nn.Module):
 
     def forward(self, hidden):
         """hidden token-major (rows, d)."""
-        h = mf.layer_norm(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
+        # (LN(x), x): the residual path's gradient is summed inside the LayerNorm backward
+        h, hidden = mf.layer_norm_skip(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
         return mf.mlp(h, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual=hidden,
                       act=self._act, p_mid=self.drop.p, p_out=self.drop.p, training=self.training)

@@ -46,8 +46,10 @@ class PreNormLunaBlock(nn.Module):
         """hidden (B*HW, d), aux (B*K, a) -> (hidden', aux', attn1 (B,nh,K,HW), attn2 (B,nh,HW,K))."""
         d, nh, qk = self.hidden_dim, self.num_heads, self.qk_proj_dim
         tr = self.training
-        aux_n = mf.layer_norm(aux, self.aux_norm.weight, self.aux_norm.bias, self.aux_norm.eps, out_b16=True)
-        hidden_n = mf.layer_norm(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
+        # (LN(x), x) pairs: the residual paths' gradients are summed inside the LayerNorm backward
+        aux_n, aux = mf.layer_norm_skip(aux, self.aux_norm.weight, self.aux_norm.bias, self.aux_norm.eps,
+                                        out_b16=True)
+        hidden_n, hidden = mf.layer_norm_skip(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
         q1 = mf.linear(aux_n, self.q1_proj.weight, self.q1_proj.bias)                       # (B*K, qk)
         w_h = torch.cat([self.k1_proj.weight, self.v1_proj.weight, self.q2_proj.weight])
         b_h = torch.cat([self.k1_proj.bias, self.v1_proj.bias, self.q2_proj.bias])

@@ -31,7 +31,7 @@ class SelfAttentionBlock(nn.Module):
     def forward(self, hidden, B, S):
         """hidden (B*S, d) -> (hidden', attn (B, nh, S, S))."""
         kq, d, nh = self.key_query_dim, self.hidden_dim, self.num_heads
-        h = mf.layer_norm(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
+        h, hidden = mf.layer_norm_skip(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
         w = torch.cat([self.query_proj.weight, self.key_proj.weight, self.value_proj.weight])
         b = torch.cat([self.query_proj.bias, self.key_proj.bias, self.value_proj.bias])
         qkv = mf.linear(h, w, b)
