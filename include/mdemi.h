@@ -164,8 +164,8 @@ int mdemi_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 int mdemi_add16(const float* a, const float* b, float* y, void* y16, int64_t n, void* stream);
 /* 1 when mdemi_gemm_bf16x would take the bf16-operand path for this descriptor. */
 int mdemi_gemm_bf16x_supported(const mdemi_gemm_desc* d, const void* a16, const void* b16);
-/* tuning hook of the bf16-operand family: 0 = 128-row tile, 1 = 256-row tile, -1 = per-shape
- * autotune (default; bit-identical). */
+/* tuning hook of the bf16-operand family: 0 = 128-row tile, 1 = 256-row tile, 2 = 128-row tile
+ * with two K tiles per LDS stage, -1 = per-shape autotune (default; all bit-identical). */
 int mdemi_gemm_set_variant_b16(int32_t variant);
 /* tuning hook: pipelining variant (0..5, see gemm_f32.hip; -1 = time the
  * candidates once per distinct shape and cache the winner, the default -- all

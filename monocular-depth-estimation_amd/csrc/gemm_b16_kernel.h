@@ -214,12 +214,16 @@ struct B16RowImg {
 };
 
 // BMT: block-tile rows (128: 2x2 waves of 64x64; 256: 2x2 waves of 128x64, A as two
-// 128-row images).  OCC: waves per SIMD the register budget targets.
-template <int AL, int BL, int BMT, int OCC>
+// 128-row images).  OCC: waves per SIMD the register budget targets.  KT2: K tiles per LDS
+// stage (1, or 2 for 128-row tiles: 16 MFMAs per wave between barriers instead of 8, for the
+// small GEMMs whose per-tile fixed cost dominates); the tiles still run in k order.
+template <int AL, int BL, int BMT, int OCC, int KT2 = 1>
 __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void gemm_b16_kernel(
     GemmParams p) {
   constexpr int NA = BMT / 128, IM = BMT / 64, WTM = BMT / 2;
-  constexpr int STAGE = (NA + 1) * B16_IMG;
+  static_assert(KT2 == 1 || (KT2 == 2 && NA == 1), "two K tiles per stage: 128-row tiles");
+  constexpr int TILE = (NA + 1) * B16_IMG;  // one K tile's images
+  constexpr int STAGE = KT2 * TILE;
   constexpr bool AROW = B16RowImg<AL, true>::v, BROW = B16RowImg<BL, false>::v;
   // stage 0 is `smem` (the epilogue's split-K hand-off flag reuses it after the loop)
   __shared__ __attribute__((aligned(16))) char smem[STAGE];
@@ -277,8 +281,7 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   // (k steps kk = 0, 1 in order, as the m16 family).  The stages are separate __shared__
   // objects named at compile time (unrolled by two), so the fragment reads of one stage are
   // not ordered behind the DMA in flight into the other.
-  auto tile = [&](int kt, const char* cur, char* nxt) {
-    if (kt + 1 < kt_end) issue(kt + 1, nxt);
+  auto compute = [&](const char* cur) {
     const char* a_s = cur + aimg * B16_IMG;
     const char* b_s = cur + NA * B16_IMG;
     b16x8_t fa[2][IM], fb[2][2];
@@ -297,17 +300,27 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 #pragma unroll
         for (int in = 0; in < 2; ++in)
           acc[im][in] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[kk][im], fb[kk][in], acc[im][in], 0, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt+1 has landed
+  };
+  // a stage holds K tiles kt .. kt + KT2 - 1 (those below kt_end; the condition is wave-uniform)
+  auto issue_stage = [&](int kt, char* st) {
+    issue(kt, st);
+    if (KT2 == 2 && kt + 1 < kt_end) issue(kt + 1, st + TILE);
+  };
+  auto tile = [&](int kt, const char* cur, char* nxt) {
+    if (kt + KT2 < kt_end) issue_stage(kt + KT2, nxt);
+    compute(cur);
+    if (KT2 == 2 && kt + 1 < kt_end) compute(cur + TILE);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the next stage has landed
     __syncthreads();                                   // ... every wave's, and `cur` is no longer read
   };
 
-  if (kt_begin < kt_end) issue(kt_begin, smem);
+  if (kt_begin < kt_end) issue_stage(kt_begin, smem);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int kt = kt_begin; kt < kt_end; kt += 2) {
+  for (int kt = kt_begin; kt < kt_end; kt += 2 * KT2) {
     tile(kt, smem, smem1);
-    if (kt + 1 >= kt_end) break;
-    tile(kt + 1, smem1, smem);
+    if (kt + KT2 >= kt_end) break;
+    tile(kt + KT2, smem1, smem);
   }
 
 #define EP_IM IM
@@ -315,12 +328,14 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 #include "gemm_epilogue.inc"
 }
 
-// variants (gemm_f32.hip, mode GEMM_B16): 0 = 128-row tile (3 waves/SIMD), 1 = 256-row tile
+// variants (gemm_f32.hip, mode GEMM_B16): 0 = 128-row tile (3 waves/SIMD), 1 = 256-row tile,
+// 2 = 128-row tile with two K tiles per stage (2 waves/SIMD); all the same k order
 template <int AL, int BL>
 static void (*pick_b16(int v))(GemmParams) {
   switch (v) {
     case 0: return gemm_b16_kernel<AL, BL, 128, 3>;
     case 1: return gemm_b16_kernel<AL, BL, 256, 2>;
+    case 2: return gemm_b16_kernel<AL, BL, 128, 2, 2>;
     default: return nullptr;
   }
 }

@@ -117,7 +117,7 @@ static bool env_on(const char* name) {
 static bool g_tail_split = env_on("MDEMI_GEMM_TAIL_SPLIT");
 static bool g_inline_reduce = env_on("MDEMI_GEMM_INLINE_REDUCE");
 static int g_variant_m16 = -1;  // 16-bit family (bf16 / split fp32): 0 two LDS buffers, 1 one
-static int g_variant_b16 = -1;  // bf16-operand family: 0 128-row tile, 1 256-row tile
+static int g_variant_b16 = -1;  // bf16-operand family: 0 128-row tile, 1 256-row tile, 2 128-row x 2 K tiles
 static int g_group_m = 8;
 
 KernelFn f32_pick_part0(int al, int bl, int aop, int bop, int v);
@@ -444,7 +444,7 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode, co
   static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11};
   static const int cands_m16[] = {0, 1, 2, 3, 4};
   const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
-  int ncand = mode == GEMM_BF16 ? 5 : mode == GEMM_F32E ? 3 : mode == GEMM_B16 ? 2 : 11;
+  int ncand = mode == GEMM_BF16 ? 5 : mode == GEMM_F32E ? 3 : mode == GEMM_B16 ? 3 : 11;
   if (mode == GEMM_F32) {
     GemmParams q;
     fill_params(d, q, 0, mode);
@@ -561,7 +561,7 @@ extern "C" int mdemi_gemm_set_variant_m16(int32_t variant) {
 }
 
 extern "C" int mdemi_gemm_set_variant_b16(int32_t variant) {
-  MDEMI_REQUIRE(variant >= -1 && variant < 2, "gemm_set_variant_b16: bad variant");
+  MDEMI_REQUIRE(variant >= -1 && variant < 3, "gemm_set_variant_b16: bad variant");
   g_variant_b16 = variant;
   return MDEMI_OK;
 }

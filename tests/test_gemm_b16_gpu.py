@@ -51,7 +51,7 @@ def _check(ref, got, c16, what):
     assert torch.equal(c16, ref.to(torch.bfloat16)), what
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K", [(3000, 384, 640), (1000, 200, 136), (4736, 1024, 256), (64, 96, 40000)])
 def test_dense_layouts_bit_identical(mf, variant, M, N, K):
     from mdemi import _lib as L
@@ -81,7 +81,7 @@ def test_dense_layouts_bit_identical(mf, variant, M, N, K):
     _check(ref, got, c16, "mn x kc")
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("cin,cout,k,pad,hw,mode", [(64, 96, 3, 1, (17, 23), "zero"), (128, 64, 3, 1, (30, 40), "rep"),
                                                     (32, 40, 5, 2, (9, 12), "zero"), (256, 256, 3, 1, (60, 80), "zero")])
 def test_conv_layouts_bit_identical(mf, variant, cin, cout, k, pad, hw, mode):
@@ -110,7 +110,7 @@ def test_conv_layouts_bit_identical(mf, variant, cin, cout, k, pad, hw, mode):
         _check(ref, got, c16, "conv dgrad")
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_batched_attention_products_bit_identical(mf, variant):
     """Two-level batch (image, head) as the Luna / self-attention products issue them:
     scores = Q K^T (k-contiguous both), out = P V (V m/n-contiguous)."""
