@@ -93,6 +93,10 @@ WORKLOADS = {
     "newcrfs_kitti": dict(opt=_NEWCRFS_KITTI, model="NewCRFs-L07", h=352, w=1216,
                           workload="NewCRFs Swin-L (large07) train step, KITTI 352x1216",
                           ref_cfg="json/kitti/newcrfs/newcrfs_github_eval.json"),
+    # the reference's real KITTI train crop (dataset/depth_dataset.py:52: random 352x704 crop)
+    "newcrfs_kitti704": dict(opt=_NEWCRFS_KITTI, model="NewCRFs-L07", h=352, w=704,
+                             workload="NewCRFs Swin-L (large07) train step, KITTI 352x704 (train crop)",
+                             ref_cfg="json/kitti/newcrfs/newcrfs_github_eval.json"),
     "adabins": dict(opt=_ADABINS_NYU, model="AdaBins-B5", h=480, w=640,
                     workload="AdaBins EfficientNet-B5 train step, NYU 480x640",
                     ref_cfg="json/nyu/adabins/adabins_cham_per_batch.json"),
@@ -113,7 +117,8 @@ WORKLOADS = {
 # The default line (BASELINE.json metric, NeW-CRFs NYU) carries every other single-GPU
 # BASELINE config as a compact secondary: configs[2] (NeW-CRFs KITTI 352x1216 bs 8),
 # configs[1] (AdaBins NYU bs 16) and configs[4] at N GPUs (Depthformer v8 bf16 + hipGraph).
-SECONDARIES = {"newcrfs_kitti": 8, "adabins": 16, "depthformer_bf16": 8}
+SECONDARIES = {"newcrfs_kitti": 8, "newcrfs_kitti704": 8, "adabins": 16, "depthformer_bf16": 8}
+SECONDARY_CPU_BUDGET_S = 8.0  # each secondary's CPU baseline: a shorter sample (the headline's is 20 s)
 # HBM bytes per launch of the roofline kernel family, from the committed
 # rocprofv3 --pmc passes (tools/pmc_traffic.py; FETCH_SIZE doubled per the
 # gfx950 correction).  None when no profile matches the kernel.
@@ -513,7 +518,7 @@ def _usable_cpus():
     return n
 
 
-def cpu_baseline(model, opt, H, W, budget_s):
+def cpu_baseline(model, opt, H, W, budget_s, all_cores=True):
     """The oracle (CPU restatement of the reference path: oracle/newcrfs.py, oracle/adabins.py,
     oracle/depthformer.py) timed on the host cores: fp32 forward + loss + backward + clipped
     AdamW step at batch 1 with the same weights, 2 warm-up steps, then as many timed steps
@@ -595,7 +600,7 @@ def cpu_baseline(model, opt, H, W, budget_s):
     allc = _usable_cpus()
     _progress(f"cpu_baseline: {threads} threads {1.0 / dt:.3f} img/s; usable CPUs {allc}")
     res["usable_cpus"] = allc
-    if allc > threads and budget_s > 0:
+    if all_cores and allc > threads and budget_s > 0:
         dt2, n2 = timed(allc, budget_s / 2)
         res["all_cores"] = {"value": round(1.0 / dt2, 4), "cores": allc, "timed_steps": n2}
     torch.set_num_threads(threads)
@@ -647,14 +652,59 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
         iso = (time.perf_counter() - t0) / 3 * 1e3
         res["allreduce"] = {"grad_bytes": sum(ddp.bucket_bytes), "buckets": len(ddp.buckets),
                             "isolated_ms": round(iso, 2), "share_of_step_upper_bound": round(iso / res["ms"], 4),
-                            "bus_GBps": round(2 * (world - 1) / world * sum(ddp.bucket_bytes) / (iso * 1e-3) / 1e9, 1),
+                            "bus_GBps": (round(2 * (world - 1) / world * sum(ddp.bucket_bytes) / (iso * 1e-3) / 1e9, 1)
+                                         if world > 1 else None),
                             "last_launch_order": ddp.last_launch_order}
+        res["allreduce"]["overlap"] = ddp_overlap(trainer, batches)
     _progress(f"{key}: {res['ms']:.1f} ms/step")
     if with_roofline:
         res["roofline"], res["extra"] = roofline_entry(trainer, batches, key, res["ms"])
         if getattr(trainer, "_hbm_kernels", None):
             res["extra"]["hbm_kernels"] = trainer._hbm_kernels
     return res
+
+
+XGMI_RING_BUS_GBPS = 300.0  # assumed RCCL ring bus bandwidth over xGMI at 8 GPUs
+
+
+def ddp_overlap(trainer, batches, n_model=8, bus_gbps=XGMI_RING_BUS_GBPS):
+    """One traced eager step (GradAllReduce.trace_events): for every bucket, when it became
+    ready and when it was launched (strict index order), in ms before the end of backward, from
+    HIP events on the compute stream.  From those offsets, the exposed communication an
+    n_model-GPU ring would leave: bucket i's all-reduce takes 2 (n-1)/n bytes_i / bus on the one
+    communication stream, starting at max(its launch, the previous bucket's end); whatever runs
+    past the end of backward is exposed."""
+    from mdemi import functional as mf
+    ddp = trainer.ddp
+    ddp.trace_events = True
+    ddp.reset()
+    try:
+        with mf.matmul_precision(trainer.precision):
+            trainer._eager_step(batches)
+        torch.cuda.synchronize()
+        tr = ddp.trace_offsets()
+    finally:
+        ddp.trace_events = False
+        ddp.reset()
+    if tr is None:
+        return None
+    t_free, exposed_by = None, []
+    for row in tr["buckets"]:  # times relative to the end of backward (negative = before it)
+        start = -row["launch_before_end_ms"]
+        if t_free is not None:
+            start = max(start, t_free)
+        dur = 2.0 * (n_model - 1) / n_model * row["bytes"] / (bus_gbps * 1e9) * 1e3
+        t_free = start + dur
+        row["model_ring_ms"] = round(dur, 3)
+        row["model_done_after_end_ms"] = round(t_free, 3)
+    exposed = max(0.0, t_free)
+    late = [r["bucket"] for r in tr["buckets"] if r["launch_before_end_ms"] < r["ready_before_end_ms"] - 0.05]
+    return {"buckets": tr["buckets"], "ready_order": tr["ready_order"],
+            "ready_order_is_index_order": tr["ready_order"] == sorted(tr["ready_order"]),
+            "held_back_buckets": late,
+            "model": f"{n_model}-GPU ring all-reduce at {bus_gbps:g} GB/s bus, buckets serialised on one "
+                     "communication stream from their measured launch times",
+            "model_exposed_ms": round(exposed, 3)}
 
 
 def measure_secondary(args, sk, rank, world, device):
@@ -670,11 +720,16 @@ def measure_secondary(args, sk, rank, world, device):
     sub.warmup = max(3 if graph else 1, min(args.warmup, 3))  # a captured step: 2 eager + the capture
     sec = measure(sub, wk["opt"], sk, wk["h"], wk["w"], B, rank, world, device, with_roofline=not args.no_roofline,
                   precision=prec, graph=graph)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(sec["trainer"].model, wk["opt"], wk["h"], wk["w"], SECONDARY_CPU_BUDGET_S, all_cores=False)
+        if prec != "fp32":
+            cpu["sample"] += " (fp32: the CPU path has no bf16 GEMM; the GPU line is bf16)"
     del sec["trainer"]
     out = {"workload": wk["workload"], "reference_config": wk["ref_cfg"], "per_gpu_batch": B,
            "image": [wk["h"], wk["w"]], "matmul_precision": prec, "hipgraph": graph, "steps": sub.steps,
            "images_per_sec": round(sec["images"] / sec["elapsed"], 3), "ms_per_step": round(sec["ms"], 2),
-           "loss": round(sec["loss"], 5)}
+           "loss": round(sec["loss"], 5), "cpu_baseline": cpu}
     if "roofline" in sec:
         out["roofline"] = sec["roofline"]
         out["step_mfma_frac"] = sec["extra"]["step_mfma_frac"]
@@ -687,6 +742,50 @@ def measure_secondary(args, sk, rank, world, device):
     if "allreduce" in sec:
         out["allreduce"] = sec["allreduce"]
     return out
+
+
+def measure_configs0(args, device, budget_s):
+    """BASELINE configs[0]: AdaBins EfficientNet-B5 forward on one 640x480 NYU crop.  The
+    reference states it as a PyTorch-CPU plumbing case; here the oracle's fp32 forward (the CPU
+    restatement, oracle/adabins.py) is timed on the host cores beside the libmdemi eval forward
+    of the same weights on the GPU (batch 1, no autograd)."""
+    from mdemi.train.builder import build_model
+    from oracle import adabins as oab
+    opt = copy.deepcopy(_ADABINS_NYU)
+    dmin, dmax = opt["eval"]["min_depth_eval"], opt["eval"]["max_depth_eval"]
+    torch.manual_seed(0)
+    model = build_model(opt).to(device).eval()
+    img, _ = synthetic_batch(1, 480, 640, device, seed=1)
+    with torch.no_grad():
+        for _ in range(3):
+            model(img)
+        torch.cuda.synchronize()
+        n = 20
+        t0 = time.perf_counter()
+        for _ in range(n):
+            model(img)
+        torch.cuda.synchronize()
+        gpu_dt = (time.perf_counter() - t0) / n
+    threads = min(CPU_SHARE_PER_GPU, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    P = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
+    cimg = img.cpu()
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        oab.unet_adaptive_bins(P, cimg, dmin, dmax)  # warm-up
+        per = time.perf_counter() - t0
+        k = max(1, min(5, int(budget_s / max(per, 1e-3))))
+        t0 = time.perf_counter()
+        for _ in range(k):
+            oab.unet_adaptive_bins(P, cimg, dmin, dmax)
+        cpu_dt = (time.perf_counter() - t0) / k
+    _progress(f"configs[0]: GPU forward {gpu_dt * 1e3:.2f} ms, CPU oracle forward {cpu_dt * 1e3:.0f} ms")
+    return {"workload": "AdaBins EfficientNet-B5 forward (eval), one NYU 480x640 crop (BASELINE configs[0])",
+            "reference_config": "json/nyu/adabins/adabins_cham_per_batch.json",
+            "gpu_images_per_sec": round(1.0 / gpu_dt, 2), "gpu_ms_per_image": round(gpu_dt * 1e3, 3),
+            "cpu_baseline": {"value": round(1.0 / cpu_dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+                             "sample": f"oracle adabins fp32 forward, batch 1 at 480x640, {k} timed after 1 warm-up, "
+                                       f"{threads} threads, CPU: {_cpu_model()}"}}
 
 
 # --------------------------------------------------------------------------- plumbing (CPU)
@@ -823,6 +922,9 @@ def main():
             if sk not in SECONDARIES:
                 raise SystemExit(f"bench: unknown secondary {sk!r}")
             secondary[sk] = measure_secondary(args, sk, rank, world, device)
+            torch.cuda.empty_cache()
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            secondary["configs0_adabins_forward"] = measure_configs0(args, device, SECONDARY_CPU_BUDGET_S)
             torch.cuda.empty_cache()
 
     if rank == 0:

@@ -79,6 +79,11 @@ class GradAllReduce:
         self.last_launch_order: list[int] = []
         self._works = []
         self._sync = True
+        # trace_events: record a HIP event on the compute stream when each bucket becomes ready
+        # (its last gradient landed) and when it is launched, and one at the end of backward
+        # (finish) -- bench.py --ddp reports the offsets (eager steps only, never in a capture)
+        self.trace_events = False
+        self.trace = None
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
         self.reset()
 
@@ -122,6 +127,24 @@ class GradAllReduce:
         self._next = 0
         self._works = []
         self.launch_order = []
+        tracing = (self.trace_events and self.flat[0].is_cuda
+                   and not torch.cuda.is_current_stream_capturing())
+        self._trace = ({"ready": [None] * len(self.buckets), "launch": [None] * len(self.buckets),
+                        "ready_order": [], "end": None} if tracing else None)
+
+    def trace_offsets(self):
+        """After a traced step (trace_events on; call after synchronising): per bucket, the ms
+        from its readiness and from its launch to the end of backward, its bytes, and the
+        order buckets became ready in."""
+        tr = self.trace
+        if tr is None or tr["end"] is None:
+            return None
+        end = tr["end"]
+        rows = [{"bucket": i, "bytes": self.bucket_bytes[i],
+                 "ready_before_end_ms": round(tr["ready"][i].elapsed_time(end), 3),
+                 "launch_before_end_ms": round(tr["launch"][i].elapsed_time(end), 3)}
+                for i in range(len(self.buckets))]
+        return {"buckets": rows, "ready_order": list(tr["ready_order"])}
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -142,18 +165,32 @@ class GradAllReduce:
             return
         bi = self.bucket_of[p]
         self._pending[bi] -= 1
+        if self._trace is not None and self._pending[bi] == 0:
+            self._trace["ready"][bi] = self._event()
+            self._trace["ready_order"].append(bi)
         # launch every ready bucket in index order (identical collective sequence on all ranks)
         while self._next < len(self.buckets) and self._pending[self._next] == 0:
             bi = self._next
             self.launch_order.append(bi)
+            if self._trace is not None:
+                self._trace["launch"][bi] = self._event()
             self._works.append(dist.all_reduce(self.flat[bi], group=self.group, async_op=True))
             self._next += 1
+
+    @staticmethod
+    def _event():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        return e
 
     def finish(self):
         """Wait for the bucket all-reduces and turn the sums into means (in place)."""
         if any(n != 0 for n in self._pending):
             missing = [bi for bi, n in enumerate(self._pending) if n != 0]
             raise RuntimeError(f"GradAllReduce: buckets {missing} never completed (unused parameters?)")
+        if self._trace is not None:
+            self._trace["end"] = self._event()
+            self.trace = self._trace
         for w in self._works:
             w.wait()
         if self.world > 1 and self.scale_in_finish:

@@ -43,13 +43,20 @@ def compute_grads():
         if perturb:
             x = x * (1 + 2.0 ** -22 * torch.from_numpy(rng_array(tuple(x.shape), 99)).double())
         with (bf16emu.enabled() if emulate else contextlib.nullcontext()), bnmode.eval_bn():
-            d, _, _ = odf.depthformer_v8_full(P, x.to(dtype), OPT, 1e-3, 10.0)
+            d, c, a = odf.depthformer_v8_full(P, x.to(dtype), OPT, 1e-3, 10.0)
             assert d.shape == dy.shape
             (d * dy.to(dtype)).sum().backward()
-        return {k: p.grad.detach().double() for k, p in P.items() if torch.is_tensor(p) and p.grad is not None}
+        outs = [t.detach().double() for t in [d, c] + list(a)]
+        return {k: p.grad.detach().double() for k, p in P.items() if torch.is_tensor(p) and p.grad is not None}, outs
 
-    return {"o64": run(torch.float64, True), "o32": run(torch.float32, True),
-            "draw": run(torch.float32, True, perturb=True), "plain": run(torch.float64, False)}
+    res = {"o64": run(torch.float64, True), "o32": run(torch.float32, True),
+           "draw": run(torch.float32, True, perturb=True), "plain": run(torch.float64, False)}
+    out = {k: v[0] for k, v in res.items()}
+    out["outputs"] = {k: v[1] for k, v in res.items()}
+    return out
+
+
+OUT_NAMES = ["depth", "centers"] + [f"attn{k}" for k in range(8)]
 
 
 def test_independent_draw_passes(grads):
@@ -70,6 +77,76 @@ def test_scaled_luna_gradient_fails(grads, proj):
     wrong[k] = wrong[k] * 1.05
     r = C.judge(wrong, grads["o64"], grads["o32"], grads["plain"])
     assert [b[0] for b in r["bad"]] == [k], r["bad"]
+
+
+def test_independent_draw_outputs_pass(grads):
+    o = grads["outputs"]
+    assert len(o["draw"]) == len(OUT_NAMES)
+    r = C.judge_outputs(OUT_NAMES, o["draw"], o["o64"], o["o32"])
+    print(f"outputs, worst: {r['rows'][:3]}")
+    assert not r["bad"], r["bad"]
+
+
+@pytest.mark.parametrize("which", ["depth", "centers"])
+def test_output_off_by_two_percent_fails(grads, which):
+    """The depth map or the bin centres scaled by 1.02 fail the output rule (their draws sit
+    0.04-0.16 % from o64 here)."""
+    o = grads["outputs"]
+    i = OUT_NAMES.index(which)
+    wrong = list(o["draw"])
+    wrong[i] = wrong[i] * 1.02
+    r = C.judge_outputs(OUT_NAMES, wrong, o["o64"], o["o32"])
+    assert [b[0] for b in r["bad"]] == [which], r["bad"]
+
+
+def test_attention_maps_are_noise_dominated_draws(grads):
+    """Why attention maps get the conditioned check: here the two emulations' maps differ by
+    more than 2 % (so rule (1) passes a map scaled by 1.02), as much as bf16 moves them from
+    the un-rounded model."""
+    o = grads["outputs"]
+    for k in range(8):
+        i = OUT_NAMES.index(f"attn{k}")
+        assert C._l2(o["o32"][i] - o["o64"][i]) > 5e-3 * C._l2(o["o64"][i])
+    wrong = list(o["draw"])
+    wrong[2] = wrong[2] * 1.02
+    assert not C.judge_outputs(OUT_NAMES, wrong, o["o64"], o["o32"])["bad"]
+
+
+def _attn_case(seed=3, scale=0.25):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.randn(2, 4, 96, 64, generator=g) * 2.0
+    k = torch.randn(2, 4, 80, 64, generator=g) * 2.0
+    ref = C.attention_reference(q, k, scale)
+    # what the GPU computes: fp32 logits of the exact bf16 products, fp32 softmax
+    q16, k16 = q.to(torch.bfloat16).float(), k.to(torch.bfloat16).float()
+    p32 = torch.softmax(scale * q16 @ k16.transpose(-1, -2), dim=-1)
+    return p32, ref
+
+
+def test_attention_given_inputs_passes():
+    p32, ref = _attn_case()
+    ok, rel, rows = C.judge_attention(p32, ref)
+    assert ok, (rel, rows)
+    assert rel < 1e-5
+
+
+@pytest.mark.parametrize("kind", ["scaled", "mixed", "unrounded_operands"])
+def test_attention_off_by_two_percent_fails(kind):
+    """A map scaled by 1.02, one with 2 % of each row moved to other keys (rows still sum to
+    one), and one computed from the un-rounded fp32 q / k (a kernel that skipped the bf16
+    rounding) all fail the conditioned attention check."""
+    p32, ref = _attn_case()
+    if kind == "scaled":
+        bad = p32 * 1.02
+    elif kind == "mixed":
+        bad = 0.98 * p32 + 0.02 * torch.roll(p32, 7, dims=-1)
+    else:
+        g = torch.Generator().manual_seed(3)
+        q = torch.randn(2, 4, 96, 64, generator=g) * 2.0
+        k = torch.randn(2, 4, 80, 64, generator=g) * 2.0
+        bad = torch.softmax(0.25 * q @ k.transpose(-1, -2), dim=-1)
+    ok, rel, rows = C.judge_attention(bad, ref)
+    assert not ok, (kind, rel, rows)
 
 
 def test_missing_bias_term_fails(grads):

@@ -235,10 +235,13 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
     0.9 of its size, so no end-to-end bound discriminates; its bf16 GEMMs are held one by one
     instead (test_every_bf16_gemm_of_the_configs4_step_is_exact).
 
-    Outputs (depth, centres, the 8 attention maps): max|gpu - o64| <= 20 x max|o32 - o64| +
-    1e-3 x max|o64|; depth and centres within twice the emulation's relative L2 distance from
-    plain (what bf16 costs against the fp32 model, printed for both).  depthformer_v8.py:46-75, decoder_v8.py:97-171,
-    luna_layer.py:181-259."""
+    Outputs (depth, centres, the 8 attention maps) are held to the same draw rule
+    (bf16_criterion.judge_outputs).  The attention maps are bf16-noise-dominated draws (two
+    valid emulations differ by several %), so each attention call of the forward is also
+    checked given its own inputs: the map must be softmax(scale * bf16(q) bf16(k)^T) of the q /
+    k the GPU computed, to 1e-3 relative L2, rows summing to 1 (bf16_criterion.
+    judge_attention; a 2 % error fails it, tests/test_bf16_criterion.py).
+    depthformer_v8.py:46-75, decoder_v8.py:97-171, luna_layer.py:181-259."""
     import contextlib
 
     import bf16_criterion as crit
@@ -259,8 +262,23 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
         if isinstance(mod, torch.nn.BatchNorm2d):
             mod.eval()
     img = torch.from_numpy(rng_array((2, 3, 480, 640), 84))
+    calls = []
+    orig_attention = mf.attention
+
+    def capture(qsrc, ksrc, vsrc, B, Sq, Sk, heads, dqk, dv, scale, q_off=0, k_off=0, **kw):
+        out, P = orig_attention(qsrc, ksrc, vsrc, B, Sq, Sk, heads, dqk, dv, scale, q_off=q_off, k_off=k_off, **kw)
+        q = qsrc.detach().view(B, Sq, -1)[..., q_off:q_off + heads * dqk].reshape(B, Sq, heads, dqk)
+        k = ksrc.detach().view(B, Sk, -1)[..., k_off:k_off + heads * dqk].reshape(B, Sk, heads, dqk)
+        calls.append((q.permute(0, 2, 1, 3).cpu(), k.permute(0, 2, 1, 3).cpu(), float(scale), P.detach().cpu()))
+        return out, P
+
+    mf.attention = capture
+    try:
+        with mf.matmul_precision("bf16"):
+            depth, centers, attn = m(img.float().to(DEV))
+    finally:
+        mf.attention = orig_attention
     with mf.matmul_precision("bf16"):
-        depth, centers, attn = m(img.float().to(DEV))
         dy = torch.from_numpy(rng_array(tuple(depth.shape), 85))
         (depth * dy.float().to(DEV)).sum().backward()
     torch.cuda.synchronize()
@@ -280,13 +298,18 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
     o32, G32 = oracle(torch.float32, True)
     plain, Gplain = oracle(torch.float64, False)
 
-    worst = []
-    for k, g, r64, r32 in zip(names, gpu_out, o64, o32):
-        e_gpu = (g.detach().double().cpu() - r64).abs().max().item()
-        e_cpu = (r32.double() - r64).abs().max().item()
-        mag = r64.abs().max().item()
-        assert e_gpu <= 20.0 * e_cpu + 1e-3 * mag + 1e-12, (k, e_gpu, e_cpu, mag)
-        worst.append((e_gpu / (mag + 1e-300), k))
+    ro = crit.judge_outputs(names, gpu_out, o64, o32)
+    for ratio, k, err, bound in ro["rows"]:
+        print(f"  output {k:10s} |gpu-o64| {err:.3e} bound {bound:.3e} ({ratio:.2f} of it)")
+    assert not ro["bad"], ro["bad"]
+    assert len(calls) >= 8, len(calls)
+    att = []
+    for q, k, scale, P in calls:
+        ok, rel, rows = crit.judge_attention(P, crit.attention_reference(q, k, scale))
+        att.append((rel, rows, tuple(P.shape)))
+        assert ok, (tuple(P.shape), rel, rows)
+    print(f"  {len(calls)} attention calls given their own q/k: worst relative L2 {max(a[0] for a in att):.2e}, "
+          f"worst row-sum error {max(a[1] for a in att):.2e}")
     params = dict(m.named_parameters())
     assert set(G64) == set(params), set(params) ^ set(G64)
     gpu = {k: p.grad.detach().double().cpu() for k, p in params.items()}
@@ -310,14 +333,8 @@ def test_depthformer_v8_480x640_bf16_vs_fp64_oracle(mf):
 
     cost = {k: rel_l2(g, ref) for k, g, ref in zip(names, gpu_out, plain)}
     emu_cost = {k: rel_l2(r, ref) for k, r, ref in zip(names, o64, plain)}
-    print(f"configs[4] bf16: worst max-error / magnitude vs the bf16-emulating fp64 oracle "
-          f"{sorted(worst, reverse=True)[:5]}; relative L2 vs the fp32-numerics fp64 oracle: GPU {cost}, "
-          f"bf16 emulation {emu_cost}")
-    # what bf16 costs against the fp32 model is the model's, not the kernels': the GPU's distance
-    # from the un-rounded model stays within twice the emulation's (peaked bin probabilities
-    # make the depth itself move ~1.5 % under bf16 here)
-    for k in ("depth", "centers"):
-        assert cost[k] <= 2.0 * emu_cost[k] + 1e-3, (k, cost[k], emu_cost[k])
+    # informational: what bf16 costs against the un-rounded fp64 model, GPU and emulation
+    print(f"configs[4] bf16: relative L2 vs the fp32-numerics fp64 model: GPU {cost}, bf16 emulation {emu_cost}")
 
 
 def test_every_bf16_gemm_of_the_configs4_step_is_exact(mf):

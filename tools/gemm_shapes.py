@@ -44,8 +44,9 @@ def main():
         split = kw.get("split_k")
         if split is None:
             split = mf._split_for(M, N, K)
-        key = (kw.get("a_layout"), kw.get("b_layout"), kw.get("a_op", 0), M, N, K, kw.get("batch", 1), split)
-        recs.append((key, s, e))
+        path = mf.LAST_GEMM[0]
+        key = (kw.get("a_layout"), kw.get("b_layout"), kw.get("a_op", 0), M, N, K, kw.get("batch", 1), split, path)
+        recs.append((key, s, e, bench._gemm_alg_bytes(A, B, M, N, K, kw, ob=2.0 if path == "b16" else 4.0)))
         return out
 
     mf.gemm = timed
@@ -54,22 +55,24 @@ def main():
         torch.cuda.synchronize()
     finally:
         mf.gemm = orig
-    by = collections.defaultdict(lambda: [0.0, 0])
-    for key, s, e in recs:
+    by = collections.defaultdict(lambda: [0.0, 0, 0.0])
+    for key, s, e, nb in recs:
         by[key][0] += s.elapsed_time(e) * 1e-3
         by[key][1] += 1
+        by[key][2] += nb
     tot_t = sum(v[0] for v in by.values())
     tot_f = sum(2.0 * k[3] * k[4] * k[5] * k[6] * v[1] for k, v in by.items())
     print(f"{len(recs)} GEMM calls, {tot_t * 1e3:.2f} ms, {tot_f / tot_t / 1e12:.1f} TF/s")
     rows = []
-    for k, (t, n) in by.items():
+    for k, (t, n, nb) in by.items():
         fl = 2.0 * k[3] * k[4] * k[5] * k[6] * n
-        lost = t - fl / 157.3e12
-        rows.append((lost, k, t, n, fl / t / 1e12))
+        peak = 2500e12 if k[8] in ("b16", "bf16") else 157.3e12
+        lost = t - max(fl / peak, nb / 8e12)  # time above the tighter of the MFMA and HBM floors
+        rows.append((lost, k, t, n, fl / t / 1e12, nb / t / 1e9))
     rows.sort(reverse=True)
-    print("lost_ms  time_ms calls   TF/s  (a_layout,b_layout,a_op,M,N,K,batch,split)")
-    for lost, k, t, n, tf in rows[:45]:
-        print(f"{lost * 1e3:7.2f} {t * 1e3:8.2f} {n:5d} {tf:6.1f}  {k}")
+    print("lost_ms  time_ms calls  us/call   TF/s   GB/s  (a_layout,b_layout,a_op,M,N,K,batch,split,path)")
+    for lost, k, t, n, tf, gbs in rows[:int(os.environ.get("SHAPES_TOP", "60"))]:
+        print(f"{lost * 1e3:7.2f} {t * 1e3:8.2f} {n:5d} {t / n * 1e6:8.1f} {tf:6.1f} {gbs:6.0f}  {k}")
 
 
 if __name__ == "__main__":

@@ -2,17 +2,20 @@
 (steps are delimited by the single adamw_kernel dispatch that ends each one; the warm-up
 steps, which include the GEMM autotuning, are skipped):
 
-  python tools/step_breakdown.py <trace_dir> <warmup> [top]
+  python tools/step_breakdown.py <trace_dir> <warmup> [top] [--by-grid]
 
-Reports wall vs kernel-busy time per step, per-family totals and the top kernels."""
+Reports wall vs kernel-busy time per step, per-family totals and the top kernels
+(--by-grid: GEMM kernels keyed by name and grid size, i.e. per output-tile x split shape)."""
 import collections
 import csv
 import re
 import sys
 
 rows = sorted(csv.DictReader(open(f"{sys.argv[1]}/run_kernel_trace.csv")), key=lambda r: int(r["Dispatch_Id"]))
-warmup = int(sys.argv[2])
-top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+by_grid = "--by-grid" in sys.argv
+argv = [a for a in sys.argv if a != "--by-grid"]
+warmup = int(argv[2])
+top = int(argv[3]) if len(argv) > 3 else 40
 adam_idx = [i for i, r in enumerate(rows) if re.search(r"adamw(_dev)?_kernel", r["Kernel_Name"])]
 lo, hi = adam_idx[warmup - 1] + 1, adam_idx[-1] + 1
 steps = len(adam_idx) - warmup
@@ -23,6 +26,8 @@ for r in win:
     d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     name = re.sub(r"\(.*", "", r["Kernel_Name"])
     name = re.sub(r"^void ", "", name)
+    if by_grid and "gemm_" in name:
+        name = f"{name} grid {int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])}"
     by[name][0] += d
     by[name][1] += 1
     busy += d
