@@ -336,6 +336,250 @@ __global__ __launch_bounds__(256) void dwconv_dw_partial_s1(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// Stride-1 depthwise conv as TY x TX output blocks per thread (35 of the 39 MBConv blocks).
+// A block's TY + K - 1 input rows are each fetched once (SPAN = TX + K - 1 quads) and feed
+// every output row they touch, with all K*K taps of the thread's 4 channels in registers:
+// (TY+K-1)*SPAN / (TY*TX) quad loads per output quad, against K*SPAN / TX for one output row
+// (K 5: 4 vs 10).  The one-row kernels re-fetched each input row K times through L1/L2 and
+// ran at 1.2 TB/s (K 5) / 2.8 TB/s (K 3) on the configs[4] shapes (profiles/round6/).  Taps
+// accumulate in the same order as dwconv_fwd_kernel (ky ascending, then kx): bit-identical.
+// ---------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void dw_load_taps(const float* __restrict__ w, int c, float4 (&wk)[K][K]) {
+  constexpr int KK = K * K;
+  const float* w0 = w + (int64_t)c * KK;
+#pragma unroll
+  for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx)
+      wk[ky][kx] = make_float4(w0[ky * K + kx], w0[KK + ky * K + kx], w0[2 * KK + ky * K + kx],
+                               w0[3 * KK + ky * K + kx]);
+}
+
+__device__ __forceinline__ void fma4(float4& a, const float4& v, const float4& w) {
+  a.x = fmaf(v.x, w.x, a.x);
+  a.y = fmaf(v.y, w.y, a.y);
+  a.z = fmaf(v.z, w.z, a.z);
+  a.w = fmaf(v.w, w.w, a.w);
+}
+
+template <int K, int TX, int TY>
+__global__ __launch_bounds__(256) void dwconv_fwd_s1_blk(const float* __restrict__ x, const float* __restrict__ w,
+                                                         float* __restrict__ y, int N, int H, int W, int C, int pad_t,
+                                                         int pad_l, int OH, int OW) {
+  constexpr int SPAN = TX + K - 1, ROWS = TY + K - 1;
+  const int C4 = C >> 2, OWT = (OW + TX - 1) / TX, OHT = (OH + TY - 1) / TY;
+  const int64_t total = (int64_t)N * OHT * OWT * C4;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c4 = (int)(e % C4);
+    int64_t t = e / C4;
+    const int oxt = (int)(t % OWT); t /= OWT;
+    const int oyt = (int)(t % OHT);
+    const int n = (int)(t / OHT);
+    const int c = c4 * 4, ox0 = oxt * TX, oy0 = oyt * TY, ix0 = ox0 - pad_l;
+    float4 wk[K][K];
+    dw_load_taps<K>(w, c, wk);
+    float4 acc[TY][TX];
+#pragma unroll
+    for (int r = 0; r < TY; ++r)
+#pragma unroll
+      for (int q = 0; q < TX; ++q) acc[r][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ri = 0; ri < ROWS; ++ri) {  // input row oy0 - pad_t + ri: tap row ky = ri - r of output row r
+      const int iy = oy0 - pad_t + ri;
+      if (iy < 0 || iy >= H) continue;
+      const float* row = x + (((int64_t)n * H + iy) * W) * C + c;
+      float4 v[SPAN];
+#pragma unroll
+      for (int j = 0; j < SPAN; ++j) {
+        const int ix = ix0 + j;
+        v[j] = (ix >= 0 && ix < W) ? *reinterpret_cast<const float4*>(row + (int64_t)ix * C)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const int ky = ri - r;
+        if (ky < 0 || ky >= K) continue;
+#pragma unroll
+        for (int j = 0; j < SPAN; ++j)
+#pragma unroll
+          for (int q = 0; q < TX; ++q) {
+            const int kx = j - q;
+            if (kx >= 0 && kx < K) fma4(acc[r][q], v[j], wk[ky][kx]);
+          }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      if (oy0 + r >= OH) break;
+      float* out = y + (((int64_t)n * OH + oy0 + r) * OW) * C + c;
+#pragma unroll
+      for (int q = 0; q < TX; ++q)
+        if (ox0 + q < OW) *reinterpret_cast<float4*>(out + (int64_t)(ox0 + q) * C) = acc[r][q];
+    }
+  }
+}
+
+// stride-1 input gradient, TY x TX blocks: dx[iy][ix] = sum dy[iy + pad_t - ky][ix + pad_l - kx]
+// w[ky][kx]; dy row oy0 + pad_t - (K-1) + ri serves output row r with ky = r + K - 1 - ri
+template <int K, int TX, int TY>
+__global__ __launch_bounds__(256) void dwconv_dx_s1_blk(const float* __restrict__ dy, const float* __restrict__ w,
+                                                        float* __restrict__ dx, int N, int H, int W, int C, int pad_t,
+                                                        int pad_l, int OH, int OW) {
+  constexpr int SPAN = TX + K - 1, ROWS = TY + K - 1;
+  const int C4 = C >> 2, WT = (W + TX - 1) / TX, HT = (H + TY - 1) / TY;
+  const int64_t total = (int64_t)N * HT * WT * C4;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c4 = (int)(e % C4);
+    int64_t t = e / C4;
+    const int ixt = (int)(t % WT); t /= WT;
+    const int iyt = (int)(t % HT);
+    const int n = (int)(t / HT);
+    const int c = c4 * 4, ix0 = ixt * TX, iy0 = iyt * TY;
+    const int ox0 = ix0 + pad_l - (K - 1), oyb = iy0 + pad_t - (K - 1);
+    float4 wk[K][K];
+    dw_load_taps<K>(w, c, wk);
+    float4 acc[TY][TX];
+#pragma unroll
+    for (int r = 0; r < TY; ++r)
+#pragma unroll
+      for (int q = 0; q < TX; ++q) acc[r][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ri = 0; ri < ROWS; ++ri) {
+      const int oy = oyb + ri;
+      if (oy < 0 || oy >= OH) continue;
+      const float* row = dy + (((int64_t)n * OH + oy) * OW) * C + c;
+      float4 v[SPAN];
+#pragma unroll
+      for (int j = 0; j < SPAN; ++j) {
+        const int ox = ox0 + j;
+        v[j] = (ox >= 0 && ox < OW) ? *reinterpret_cast<const float4*>(row + (int64_t)ox * C)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const int ky = r + (K - 1) - ri;
+        if (ky < 0 || ky >= K) continue;
+#pragma unroll
+        for (int j = 0; j < SPAN; ++j)
+#pragma unroll
+          for (int q = 0; q < TX; ++q) {
+            const int kx = q + (K - 1) - j;
+            if (kx >= 0 && kx < K) fma4(acc[r][q], v[j], wk[ky][kx]);
+          }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      if (iy0 + r >= H) break;
+      float* out = dx + (((int64_t)n * H + iy0 + r) * W) * C + c;
+#pragma unroll
+      for (int q = 0; q < TX; ++q)
+        if (ix0 + q < W) *reinterpret_cast<float4*>(out + (int64_t)(ix0 + q) * C) = acc[r][q];
+    }
+  }
+}
+
+// stride-1 weight gradient, TY x TX output blocks per work item: the TY*TX dy quads and the
+// TY + K - 1 input rows (SPAN quads each) are loaded once per item and update all K*K taps;
+// block = 64 channel quads x 4 item lanes over a chunk of items, partials as in
+// dwconv_dw_partial (part[chunk][c*KK + tap], a fixed-order column sum after)
+template <int K, int TX, int TY>
+__global__ __launch_bounds__(256) void dwconv_dw_partial_s1_blk(const float* __restrict__ dy,
+                                                                const float* __restrict__ x, float* __restrict__ part,
+                                                                int N, int H, int W, int C, int pad_t, int pad_l,
+                                                                int OH, int OW, int64_t grp_per_chunk, int cl) {
+  constexpr int KK = K * K, SPAN = TX + K - 1, ROWS = TY + K - 1;
+  __shared__ float4 red[256];
+  // cl channel-quad lanes x 256 / cl item lanes (cl = 64, or fewer for narrow maps: the
+  // 24/48-channel stage-0 blocks would leave 58 of 64 lanes idle)
+  const int lane = threadIdx.x % cl, ty = threadIdx.x / cl, nil = 256 / cl;
+  const int C4 = C >> 2;
+  const int c4 = blockIdx.x * cl + lane;
+  const bool cok = c4 < C4;
+  const int c = (cok ? c4 : 0) * 4;
+  const int OWT = (OW + TX - 1) / TX, OHT = (OH + TY - 1) / TY;
+  const int64_t ngrp = (int64_t)N * OHT * OWT;
+  const int64_t g0 = (int64_t)blockIdx.y * grp_per_chunk;
+  const int64_t g1 = min(ngrp, g0 + grp_per_chunk);
+  float4 acc[K][K];
+#pragma unroll
+  for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) acc[ky][kx] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (cok) {
+    for (int64_t gi = g0 + ty; gi < g1; gi += nil) {
+      const int oxt = (int)(gi % OWT);
+      const int64_t t = gi / OWT;
+      const int oyt = (int)(t % OHT);
+      const int n = (int)(t / OHT);
+      const int ox0 = oxt * TX, oy0 = oyt * TY;
+      float4 g[TY][TX];
+#pragma unroll
+      for (int r = 0; r < TY; ++r)
+#pragma unroll
+        for (int q = 0; q < TX; ++q)
+          g[r][q] = (oy0 + r < OH && ox0 + q < OW)
+                        ? *reinterpret_cast<const float4*>(dy + (((int64_t)n * OH + oy0 + r) * OW + ox0 + q) * C + c)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int ri = 0; ri < ROWS; ++ri) {
+        const int iy = oy0 - pad_t + ri;
+        if (iy < 0 || iy >= H) continue;
+        const float* row = x + (((int64_t)n * H + iy) * W) * C + c;
+        float4 v[SPAN];
+#pragma unroll
+        for (int j = 0; j < SPAN; ++j) {
+          const int ix = ox0 - pad_l + j;
+          v[j] = (ix >= 0 && ix < W) ? *reinterpret_cast<const float4*>(row + (int64_t)ix * C)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int r = 0; r < TY; ++r) {
+          const int ky = ri - r;
+          if (ky < 0 || ky >= K) continue;
+#pragma unroll
+          for (int j = 0; j < SPAN; ++j)
+#pragma unroll
+            for (int q = 0; q < TX; ++q) {
+              const int kx = j - q;
+              if (kx >= 0 && kx < K) fma4(acc[ky][kx], g[r][q], v[j]);
+            }
+        }
+      }
+    }
+  }
+  float* dst = part + (int64_t)blockIdx.y * C * KK;
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+    red[threadIdx.x] = acc[k / K][k % K];
+    __syncthreads();
+    if (ty == 0 && cok) {
+      float4 sum = red[lane];
+      for (int q = 1; q < nil; ++q) {  // item lanes in order
+        const float4 v = red[q * cl + lane];
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+      }
+      dst[(int64_t)(c + 0) * KK + k] = sum.x;
+      dst[(int64_t)(c + 1) * KK + k] = sum.y;
+      dst[(int64_t)(c + 2) * KK + k] = sum.z;
+      dst[(int64_t)(c + 3) * KK + k] = sum.w;
+    }
+    __syncthreads();
+  }
+}
+
+// tile rows per thread of the stride-1 block kernels (MDEMI_DW_TY: A/B; 1 = the one-row kernels)
+static int dw_ty() {
+  static int ty = [] {
+    const char* v = getenv("MDEMI_DW_TY");
+    const int t = v ? atoi(v) : 4;
+    return (t == 1 || t == 2 || t == 4) ? t : 4;
+  }();
+  return ty;
+}
+
 static int dw_chunks(int C, int64_t npix) {
   const int gx = (int)cdiv(C / 4, 64);
   int64_t ch = cdiv(1024, gx);
@@ -546,6 +790,18 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_pad_kernel(const float* __re
 template <int K, int S>
 static void launch_dw_fwd(const float* x, const float* w, float* y, int N, int H, int W, int C, int pt, int pl, int OH,
                           int OW, hipStream_t st) {
+  if (S == 1 && dw_ty() > 1) {
+    constexpr int TX = 4;
+    const int TY = dw_ty();
+    const int64_t total = (int64_t)N * ((OH + TY - 1) / TY) * ((OW + TX - 1) / TX) * (C / 4);
+    if (TY == 2)
+      hipLaunchKernelGGL((dwconv_fwd_s1_blk<K, TX, 2>), dim3(grid_1d(total)), dim3(256), 0, st, x, w, y, N, H, W, C,
+                         pt, pl, OH, OW);
+    else
+      hipLaunchKernelGGL((dwconv_fwd_s1_blk<K, TX, 4>), dim3(grid_1d(total)), dim3(256), 0, st, x, w, y, N, H, W, C,
+                         pt, pl, OH, OW);
+    return;
+  }
   constexpr int TX = S == 1 ? 4 : 2;
   const int64_t total = (int64_t)N * OH * ((OW + TX - 1) / TX) * (C / 4);
   hipLaunchKernelGGL((dwconv_fwd_kernel<K, S, TX>), dim3(grid_1d(total)), dim3(256), 0, st, x, w, y, N, H, W, C, pt,
@@ -554,7 +810,17 @@ static void launch_dw_fwd(const float* x, const float* w, float* y, int N, int H
 template <int K, int S>
 static void launch_dw_bwd(const float* dy, const float* x, const float* w, float* dx, float* part, int N, int H,
                           int W, int C, int pt, int pl, int OH, int OW, hipStream_t st) {
-  if (dx) {
+  if (dx && S == 1 && dw_ty() > 1) {
+    constexpr int TX = 4;
+    const int TY = dw_ty();
+    const int64_t total = (int64_t)N * ((H + TY - 1) / TY) * ((W + TX - 1) / TX) * (C / 4);
+    if (TY == 2)
+      hipLaunchKernelGGL((dwconv_dx_s1_blk<K, TX, 2>), dim3(grid_1d(total)), dim3(256), 0, st, dy, w, dx, N, H, W, C,
+                         pt, pl, OH, OW);
+    else
+      hipLaunchKernelGGL((dwconv_dx_s1_blk<K, TX, 4>), dim3(grid_1d(total)), dim3(256), 0, st, dy, w, dx, N, H, W, C,
+                         pt, pl, OH, OW);
+  } else if (dx) {
     constexpr int TX = 4;
     const int64_t total = (int64_t)N * H * ((W + TX - 1) / TX) * (C / 4);
     if (S == 1)
@@ -564,7 +830,22 @@ static void launch_dw_bwd(const float* dy, const float* x, const float* w, float
       hipLaunchKernelGGL((dwconv_dx_kernel<K, S, TX>), dim3(grid_1d(total)), dim3(256), 0, st, dy, w, dx, N, H, W,
                          C, pt, pl, OH, OW);
   }
-  if (part && S == 1) {
+  if (part && S == 1 && dw_ty() > 1) {
+    constexpr int TXW = 4;
+    const int TY = dw_ty();
+    const int64_t npix = (int64_t)N * OH * OW;
+    const int ch = dw_chunks(C, npix);
+    const int64_t ngrp = (int64_t)N * ((OH + TY - 1) / TY) * ((OW + TXW - 1) / TXW);
+    int cl = 8;
+    while (cl < 64 && cl < C / 4) cl *= 2;
+    dim3 grid((unsigned)cdiv(C / 4, cl), (unsigned)ch);
+    if (TY == 2)
+      hipLaunchKernelGGL((dwconv_dw_partial_s1_blk<K, TXW, 2>), grid, dim3(256), 0, st, dy, x, part, N, H, W, C, pt,
+                         pl, OH, OW, cdiv(ngrp, ch), cl);
+    else
+      hipLaunchKernelGGL((dwconv_dw_partial_s1_blk<K, TXW, 4>), grid, dim3(256), 0, st, dy, x, part, N, H, W, C, pt,
+                         pl, OH, OW, cdiv(ngrp, ch), cl);
+  } else if (part && S == 1) {
     constexpr int TXW = 4;
     const int64_t npix = (int64_t)N * OH * OW;
     const int ch = dw_chunks(C, npix);

@@ -284,22 +284,37 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   auto compute = [&](const char* cur) {
     const char* a_s = cur + aimg * B16_IMG;
     const char* b_s = cur + NA * B16_IMG;
-    b16x8_t fa[2][IM], fb[2][2];
+    if constexpr (IM == 2) {
+      b16x8_t fa[2][IM], fb[2][2];
 #pragma unroll
-    for (int i = 0; i < IM; ++i) fa[0][i] = fragA(a_s, i, 0);
-    fb[0][0] = fragB(b_s, 0, 0);
-    fb[0][1] = fragB(b_s, 1, 0);
+      for (int i = 0; i < IM; ++i) fa[0][i] = fragA(a_s, i, 0);
+      fb[0][0] = fragB(b_s, 0, 0);
+      fb[0][1] = fragB(b_s, 1, 0);
 #pragma unroll
-    for (int i = 0; i < IM; ++i) fa[1][i] = fragA(a_s, i, 1);
-    fb[1][0] = fragB(b_s, 0, 1);
-    fb[1][1] = fragB(b_s, 1, 1);
+      for (int i = 0; i < IM; ++i) fa[1][i] = fragA(a_s, i, 1);
+      fb[1][0] = fragB(b_s, 0, 1);
+      fb[1][1] = fragB(b_s, 1, 1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int im = 0; im < IM; ++im)
+        for (int im = 0; im < IM; ++im)
 #pragma unroll
-        for (int in = 0; in < 2; ++in)
-          acc[im][in] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[kk][im], fb[kk][in], acc[im][in], 0, 0, 0);
+          for (int in = 0; in < 2; ++in)
+            acc[im][in] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[kk][im], fb[kk][in], acc[im][in], 0, 0, 0);
+    } else {
+      // 256-row tile: one k step's fragments at a time (the two-step form of the 128-row tile
+      // left the compiler a private array here: 576 B of scratch, ~20x slower, round 6)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const b16x8_t b0 = fragB(b_s, 0, kk), b1 = fragB(b_s, 1, kk);
+#pragma unroll
+        for (int im = 0; im < IM; ++im) {
+          const b16x8_t a = fragA(a_s, im, kk);
+          acc[im][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0, acc[im][0], 0, 0, 0);
+          acc[im][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b1, acc[im][1], 0, 0, 0);
+        }
+      }
+    }
   };
   // a stage holds K tiles kt .. kt + KT2 - 1 (those below kt_end; the condition is wave-uniform)
   auto issue_stage = [&](int kt, char* st) {
@@ -329,7 +344,11 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 }
 
 // variants (gemm_f32.hip, mode GEMM_B16): 0 = 128-row tile (3 waves/SIMD), 1 = 256-row tile,
-// 2 = 128-row tile with two K tiles per stage (2 waves/SIMD); all the same k order
+// 2 = 128-row tile with two K tiles per stage (2 waves/SIMD); all the same k order.  (Tried in
+// round 6 and dropped: a 4/6-stage DMA ring and register staging (buffer_load_dwordx4 +
+// ds_write_b128, 1 or 2 K tiles ahead) -- neither moved the small-grid shapes, which run at
+// ~32 GB/s of operand fetch per workgroup however the fetch is issued:
+// profiles/round6/b16_variants_*.txt)
 template <int AL, int BL>
 static void (*pick_b16(int v))(GemmParams) {
   switch (v) {

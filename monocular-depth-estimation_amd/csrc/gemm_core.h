@@ -4,9 +4,23 @@
 // k-contiguous, dense m/n-contiguous, implicit-im2col NHWC), the fused
 // epilogue value and the XCD-aware tile raster.
 #pragma once
+#include <utility>
+
 #include "common.h"
 
 namespace mdemi {
+
+// f(std::integral_constant<int, i>) for i = 0 .. N-1, expanded at compile time: the epilogue
+// indexes the accumulator array with these constants, so it never depends on the unroller
+// (whose give-up on the 256-row tiles' epilogue left acc[4][2] as a private array in scratch)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
