@@ -382,6 +382,15 @@ int mdemi_bn_train_fwd16(const float* x, const float* gamma, const float* beta, 
                          float* mean, float* rstd, float* running_mean, float* running_var,
                          int64_t* num_batches_tracked, float momentum, int32_t N, int64_t HW, int32_t C,
                          float eps, int32_t act, void* workspace, void* stream);
+/* mdemi_bn_train_fwd16 that also writes pooled [N][C] = the spatial mean of y per image (the
+ * SqueezeExcite pooling of the EfficientNet block whose BatchNormAct2d output feeds its SE,
+ * gen-efficientnet via unet_adaptive_bins.py:129 / depthformer_v8.py:89) in the same sweep
+ * as y.  C % 4 == 0, 16-B aligned x / y; workspace: mdemi_bn_train_fwd_pooled_workspace_size. */
+size_t mdemi_bn_train_fwd_pooled_workspace_size(int32_t N, int64_t HW, int32_t C);
+int mdemi_bn_train_fwd_pooled(const float* x, const float* gamma, const float* beta, float* y, void* y16,
+                              float* pooled, float* mean, float* rstd, float* running_mean, float* running_var,
+                              int64_t* num_batches_tracked, float momentum, int32_t N, int64_t HW, int32_t C,
+                              float eps, int32_t act, void* workspace, void* stream);
 /* mdemi_chnorm_bwd (BatchNorm) also writing dx16 (may be NULL): the RNE bf16 copy of dx, the
  * output gradient of the conv before the BN that its data- and weight-gradient GEMMs read. */
 int mdemi_chnorm_bwd16(const float* dy, const float* x, const float* y, const float* mean,

@@ -60,11 +60,13 @@ int mdemi_chan_scale16(const float* x, const float* g, const float* add, float* 
 /* pre-activation of conv_reduce [N][R] (saved for the backward).            */
 int mdemi_se_gate_fwd(const float* pooled, const float* wr, const float* br, const float* we, const float* be,
                       float* hid, float* gate, int32_t N, int32_t C, int32_t R, void* stream);
-/* dgate [N][C] -> dpooled [N][C] and the four parameter gradients (overwritten). */
+/* dgate [N][C] -> dpooled_scale x dpooled [N][C] (1/HW: the gradient each position of the  */
+/* mean receives) and the four parameter gradients (overwritten).                           */
 size_t mdemi_se_gate_bwd_workspace_size(int32_t N, int32_t C, int32_t R);
 int mdemi_se_gate_bwd(const float* pooled, const float* wr, const float* we, const float* hid,
                       const float* gate, const float* dgate, float* dpooled, float* dwr, float* dbr, float* dwe,
-                      float* dbe, int32_t N, int32_t C, int32_t R, void* workspace, void* stream);
+                      float* dbe, int32_t N, int32_t C, int32_t R, float dpooled_scale, void* workspace,
+                      void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Row softmax with a pre-scale, y = softmax(scale * x) along the last dim:  */

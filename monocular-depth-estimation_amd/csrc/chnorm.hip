@@ -223,6 +223,8 @@ constexpr int BN_SLICE_QUADS = 64;
 struct BnGrid {
   int64_t rows, rpc;  // rows (N*H*W), rows per chunk
   int C, CQ, nsl, sq, nchunk;
+  int64_t hw;  // rows per image (with cpi > 0)
+  int cpi;     // > 0: chunks never straddle images -- cpi chunks per image, chunk = n * cpi + k
 };
 // nsl * nchunk ~= target blocks, chunks of >= 32 rows
 static BnGrid bn_grid(int64_t rows, int C, int target_blocks) {
@@ -237,6 +239,20 @@ static BnGrid bn_grid(int64_t rows, int C, int target_blocks) {
   if (nch < 1) nch = 1;
   g.rpc = cdiv(rows, nch);
   g.nchunk = (int)cdiv(rows, g.rpc);
+  g.hw = rows;
+  g.cpi = 0;
+  return g;
+}
+// image-aligned chunks (the apply that also pools each image's output, for SqueezeExcite)
+static BnGrid bn_grid_img(int N, int64_t HW, int C, int target_blocks) {
+  BnGrid g = bn_grid((int64_t)N * HW, C, target_blocks);
+  int64_t cpi = cdiv(target_blocks, (int64_t)g.nsl * N);
+  cpi = cpi < cdiv(HW, 32) ? cpi : cdiv(HW, 32);
+  if (cpi < 1) cpi = 1;
+  g.rpc = cdiv(HW, cpi);
+  g.cpi = (int)cdiv(HW, g.rpc);
+  g.nchunk = N * g.cpi;
+  g.hw = HW;
   return g;
 }
 
@@ -253,8 +269,14 @@ __device__ __forceinline__ BnLane bn_lane(const BnGrid& g) {
   L.rpt = CN_THREADS / L.sq;
   L.lane_r = threadIdx.x / L.sq;
   L.q = q0 + threadIdx.x % L.sq;
-  L.r0 = (int64_t)L.chunk * g.rpc;
-  L.r1 = min(g.rows, L.r0 + g.rpc);
+  if (g.cpi > 0) {
+    const int n = L.chunk / g.cpi, k = L.chunk - n * g.cpi;
+    L.r0 = (int64_t)n * g.hw + (int64_t)k * g.rpc;
+    L.r1 = min((int64_t)(n + 1) * g.hw, L.r0 + g.rpc);
+  } else {
+    L.r0 = (int64_t)L.chunk * g.rpc;
+    L.r1 = min(g.rows, L.r0 + g.rpc);
+  }
   return L;
 }
 // rows of this thread: r0 + lane_r, + rpt, ... < r1 (none for the idle lanes past rpt * sq)
@@ -457,38 +479,69 @@ __global__ __launch_bounds__(CN_THREADS) void bn_stats4(const float* __restrict_
   }
 }
 
+// pool_part (image-aligned grid, g.cpi > 0): also each chunk's per-channel sum of the output,
+// part[chunk][C] (rows in order per lane, lanes folded in order), which bn_pool_final turns into
+// the per-image spatial mean SqueezeExcite pools -- one read of the output fewer
 template <int ACT = -1>
 __global__ __launch_bounds__(CN_THREADS) void bn_apply4(const float* __restrict__ x, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, float* __restrict__ y,
-                                                        __bf16* __restrict__ y16, BnGrid g, int act) {
+                                                        __bf16* __restrict__ y16, BnGrid g, int act,
+                                                        float* __restrict__ pool_part) {
   constexpr int U = 4;
+  __shared__ float4 red[CN_THREADS];
   if (ACT >= 0) act = ACT;
   const BnLane L = bn_lane(g);
   const int n = bn_lane_rows(L), c = 4 * L.q;
-  if (n == 0) return;
-  const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
-  const int64_t step = (int64_t)L.rpt * g.C;
-  int64_t off = (L.r0 + L.lane_r) * g.C + c;
-  auto one = [&](float4 v, int64_t o) {
-    float4 r;
-    r.x = apply_act(act, (v.x - mu.x) * rs.x * ga.x + be.x);
-    r.y = apply_act(act, (v.y - mu.y) * rs.y * ga.y + be.y);
-    r.z = apply_act(act, (v.z - mu.z) * rs.z * ga.z + be.z);
-    r.w = apply_act(act, (v.w - mu.w) * rs.w * ga.w + be.w);
-    *reinterpret_cast<float4*>(y + o) = r;
-    if (y16) store_bf16x4(y16 + o, r);
-  };
-  int i = 0;
-  for (; i + U <= n; i += U) {
-    float4 v[U];
+  if (n == 0 && !pool_part) return;
+  float4 ps = f4(0.f);
+  if (n > 0) {
+    const float4 mu = ld4(mean + c), rs = ld4(rstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
+    const int64_t step = (int64_t)L.rpt * g.C;
+    int64_t off = (L.r0 + L.lane_r) * g.C + c;
+    auto one = [&](float4 v, int64_t o) {
+      float4 r;
+      r.x = apply_act(act, (v.x - mu.x) * rs.x * ga.x + be.x);
+      r.y = apply_act(act, (v.y - mu.y) * rs.y * ga.y + be.y);
+      r.z = apply_act(act, (v.z - mu.z) * rs.z * ga.z + be.z);
+      r.w = apply_act(act, (v.w - mu.w) * rs.w * ga.w + be.w);
+      *reinterpret_cast<float4*>(y + o) = r;
+      if (y16) store_bf16x4(y16 + o, r);
+      if (pool_part) { ps.x += r.x; ps.y += r.y; ps.z += r.z; ps.w += r.w; }
+    };
+    int i = 0;
+    for (; i + U <= n; i += U) {
+      float4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld4(x + off + u * step);
+      for (int u = 0; u < U; ++u) v[u] = ld4(x + off + u * step);
 #pragma unroll
-    for (int u = 0; u < U; ++u) one(v[u], off + u * step);
-    off += U * step;
+      for (int u = 0; u < U; ++u) one(v[u], off + u * step);
+      off += U * step;
+    }
+    for (; i < n; ++i, off += step) one(ld4(x + off), off);
   }
-  for (; i < n; ++i, off += step) one(ld4(x + off), off);
+  if (!pool_part) return;
+  red[threadIdx.x] = ps;  // fold the row lanes of each quad in lane order
+  __syncthreads();
+  if ((int)threadIdx.x < L.sq) {
+    for (int k = 1; k < L.rpt; ++k) {
+      const float4 o = red[k * L.sq + threadIdx.x];
+      ps.x += o.x; ps.y += o.y; ps.z += o.z; ps.w += o.w;
+    }
+    *reinterpret_cast<float4*>(pool_part + (int64_t)L.chunk * g.C + c) = ps;
+  }
+}
+
+// pooled[n][c] = scale * sum of the image's chunk partials, in chunk order (fp64)
+__global__ __launch_bounds__(256) void bn_pool_final(const float* __restrict__ part, float* __restrict__ out, int N,
+                                                     int C, int cpi, float scale) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)N * C) return;
+  const int n = (int)(e / C), c = (int)(e % C);
+  double s = 0.0;
+#pragma unroll 8
+  for (int k = 0; k < cpi; ++k) s += (double)part[((int64_t)n * cpi + k) * C + c];
+  out[e] = (float)(s * (double)scale);
 }
 
 template <int ACT = -1>
@@ -604,9 +657,15 @@ __global__ void bn_running_kernel(const float* __restrict__ mean, const float* _
 
 static float bn_unbias(int64_t rows) { return (float)((double)rows / (double)(rows > 1 ? rows - 1 : 1)); }
 
+static size_t bn_pool_part_bytes(int32_t N, int64_t HW, int32_t C) {
+  const BnGrid g = bn_grid_img(N, HW, C, bn_apply_blocks());
+  return align_up((size_t)g.nchunk * C * sizeof(float), 256);
+}
+
 static int chnorm_fwd_impl(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
                            int32_t N, int64_t HW, int32_t C, int32_t groups, int32_t is_bn, float eps, int32_t act,
-                           void* workspace, void* stream, BnRunning run, __bf16* y16 = nullptr) {
+                           void* workspace, void* stream, BnRunning run, __bf16* y16 = nullptr,
+                           float* pooled = nullptr, float* pool_part = nullptr) {
   MDEMI_REQUIRE(x && gamma && beta && y && mean && rstd && N > 0 && HW > 0 && C > 0, "chnorm_fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   if (is_bn) {
@@ -622,8 +681,16 @@ static int chnorm_fwd_impl(const float* x, const float* gamma, const float* beta
       hipLaunchKernelGGL(bn_stats4<0>, dim3(gs.nsl * gs.nchunk), dim3(CN_THREADS), 0, st, x, nullptr, mean, rstd, gamma,
                          beta, (double*)part, gs, act);
       hipLaunchKernelGGL(bn_reduce4<0>, dim3(gs.CQ), dim3(CN_THREADS), 0, st, (const double*)part, gs, o0);
+      if (pooled) {
+        const BnGrid gp = bn_grid_img(N, HW, C, bn_apply_blocks());
+        MDEMI_BN_ACT_LAUNCH(MDEMI_KT_APPLY4, act, dim3(gp.nsl * gp.nchunk), dim3(CN_THREADS), 0, st, x, gamma, beta,
+                            mean, rstd, y, y16, gp, act, pool_part);
+        hipLaunchKernelGGL(bn_pool_final, dim3((unsigned)cdiv((int64_t)N * C, 256)), dim3(256), 0, st, pool_part,
+                           pooled, N, C, gp.cpi, (float)(1.0 / (double)HW));
+        return check_launch("chnorm_fwd");
+      }
       MDEMI_BN_ACT_LAUNCH(MDEMI_KT_APPLY4, act, dim3(ga.nsl * ga.nchunk), dim3(CN_THREADS), 0, st, x, gamma, beta, mean,
-                          rstd, y, y16, ga, act);
+                          rstd, y, y16, ga, act, (float*)nullptr);
       return check_launch("chnorm_fwd");
     }
     const int rpb = rows_per_block(rows);
@@ -659,6 +726,27 @@ extern "C" int mdemi_bn_train_fwd(const float* x, const float* gamma, const floa
                                   void* workspace, void* stream) {
   return mdemi_bn_train_fwd16(x, gamma, beta, y, nullptr, mean, rstd, running_mean, running_var, num_batches_tracked,
                               momentum, N, HW, C, eps, act, workspace, stream);
+}
+
+extern "C" size_t mdemi_bn_train_fwd_pooled_workspace_size(int32_t N, int64_t HW, int32_t C) {
+  return align_up(mdemi_chnorm_workspace_size(N, HW, C, C, 1), 256) + bn_pool_part_bytes(N, HW, C);
+}
+
+extern "C" int mdemi_bn_train_fwd_pooled(const float* x, const float* gamma, const float* beta, float* y, void* y16,
+                                         float* pooled, float* mean, float* rstd, float* running_mean,
+                                         float* running_var, int64_t* num_batches_tracked, float momentum, int32_t N,
+                                         int64_t HW, int32_t C, float eps, int32_t act, void* workspace,
+                                         void* stream) {
+  MDEMI_REQUIRE(running_mean && running_var && pooled, "bn_train_fwd_pooled: running statistics and pooled required");
+  MDEMI_REQUIRE(C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0,
+                "bn_train_fwd_pooled: needs C %% 4 == 0 and 16-B aligned x / y (C=%d)", C);
+  MDEMI_REQUIRE(!y16 || ((uintptr_t)y16 & 7) == 0, "bn_train_fwd_pooled: y16 must be 8-B aligned");
+  if (!workspace) { set_error("bn_train_fwd_pooled: workspace required"); return MDEMI_EWORKSPACE; }
+  const int64_t rows = (int64_t)N * HW;
+  float* pool_part = (float*)((char*)workspace + align_up(mdemi_chnorm_workspace_size(N, HW, C, C, 1), 256));
+  return chnorm_fwd_impl(x, gamma, beta, y, mean, rstd, N, HW, C, C, 1, eps, act, workspace, stream,
+                         BnRunning{running_mean, running_var, num_batches_tracked, bn_unbias(rows), momentum},
+                         (__bf16*)y16, pooled, pool_part);
 }
 
 extern "C" int mdemi_bn_train_fwd16(const float* x, const float* gamma, const float* beta, float* y, void* y16,

@@ -733,7 +733,7 @@ __global__ __launch_bounds__(256) void se_dz_kernel(const float* __restrict__ we
 }
 
 __global__ __launch_bounds__(256) void se_dpooled_kernel(const float* __restrict__ wr, const float* __restrict__ dz,
-                                                         float* __restrict__ dpooled, int C, int R) {
+                                                         float* __restrict__ dpooled, int C, int R, float scale) {
   __shared__ float sdz[SE_MAXR];
   const int n = blockIdx.x;
   for (int r = threadIdx.x; r < R; r += 256) sdz[r] = dz[(int64_t)n * R + r];
@@ -742,7 +742,7 @@ __global__ __launch_bounds__(256) void se_dpooled_kernel(const float* __restrict
   if (c >= C) return;
   float s = 0.f;
   for (int r = 0; r < R; ++r) s = fmaf(wr[(int64_t)r * C + c], sdz[r], s);
-  dpooled[(int64_t)n * C + c] = s;
+  dpooled[(int64_t)n * C + c] = s * scale;  // scale 1 / HW: the per-position gradient of the mean
 }
 
 // parameter gradients, summed over the N images in order
@@ -966,8 +966,8 @@ extern "C" size_t mdemi_se_gate_bwd_workspace_size(int32_t N, int32_t C, int32_t
 
 extern "C" int mdemi_se_gate_bwd(const float* pooled, const float* wr, const float* we, const float* hid,
                                  const float* gate, const float* dgate, float* dpooled, float* dwr, float* dbr,
-                                 float* dwe, float* dbe, int32_t N, int32_t C, int32_t R, void* workspace,
-                                 void* stream) {
+                                 float* dwe, float* dbe, int32_t N, int32_t C, int32_t R, float dpooled_scale,
+                                 void* workspace, void* stream) {
   MDEMI_REQUIRE(pooled && wr && we && hid && gate && dgate && dpooled && dwr && dbr && dwe && dbe && N > 0 && C > 0 &&
                     R > 0, "se_gate_bwd: bad args");
   MDEMI_REQUIRE(C <= SE_MAXC && R <= SE_MAXR, "se_gate_bwd: C=%d R=%d exceed %d/%d", C, R, SE_MAXC, SE_MAXR);
@@ -976,7 +976,8 @@ extern "C" int mdemi_se_gate_bwd(const float* pooled, const float* wr, const flo
   float* dz = de + (int64_t)N * C;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(se_dz_kernel, dim3(N, (unsigned)cdiv(R, 4)), dim3(256), 0, st, we, hid, gate, dgate, de, dz, C, R);
-  hipLaunchKernelGGL(se_dpooled_kernel, dim3(N, (unsigned)cdiv(C, 256)), dim3(256), 0, st, wr, dz, dpooled, C, R);
+  hipLaunchKernelGGL(se_dpooled_kernel, dim3(N, (unsigned)cdiv(C, 256)), dim3(256), 0, st, wr, dz, dpooled, C, R,
+                     dpooled_scale);
   const int64_t total = 2 * (int64_t)R * C + C + R;
   hipLaunchKernelGGL(se_gate_wgrad_kernel, dim3(grid_1d(total)), dim3(256), 0, st, pooled, hid, de, dz, dwr, dbr, dwe,
                      dbe, N, C, R);

@@ -125,6 +125,9 @@ _SIGS = {
     "mdemi_add16": (ctypes.c_int, [vp, vp, vp, vp, i64, vp]),
     "mdemi_bn_train_fwd16": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i64, i32, f32, i32, vp,
                                             vp]),
+    "mdemi_bn_train_fwd_pooled_workspace_size": (sz, [i32, i64, i32]),
+    "mdemi_bn_train_fwd_pooled": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i64, i32, f32, i32,
+                                                 vp, vp]),
     "mdemi_chnorm_bwd16": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32,
                                           vp, vp]),
     "mdemi_chan_scale16": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, i64, i32, vp]),
@@ -188,7 +191,7 @@ _SIGS = {
     "mdemi_chan_scale": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, vp]),
     "mdemi_se_gate_fwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]),
     "mdemi_se_gate_bwd_workspace_size": (sz, [i32, i32, i32]),
-    "mdemi_se_gate_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "mdemi_se_gate_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp, vp]),
     "mdemi_softmax_fwd": (ctypes.c_int, [vp, vp, i64, i32, f32, vp]),
     "mdemi_softmax_bwd": (ctypes.c_int, [vp, vp, vp, i64, i32, f32, i32, vp]),
     "mdemi_softmax_fwd16": (ctypes.c_int, [vp, vp, vp, i64, i32, f32, vp]),

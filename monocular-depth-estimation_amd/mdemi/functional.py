@@ -1157,12 +1157,14 @@ def nhwc_to_nchw(x):
 
 class _ChNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, groups, is_bn, eps, act, running=None, out_b16=False):
+    def forward(ctx, x, weight, bias, groups, is_bn, eps, act, running=None, out_b16=False, pool=False):
         """running: (running_mean, running_var, num_batches_tracked or None, momentum) -- the
         BatchNorm running-statistics update done by the same call (mdemi_bn_train_fwd).
         out_b16: the output feeds a bf16 GEMM -- write its bf16 copy too (bf16 storage).  The
         input gradient gets its bf16 copy when the input came from a conv (its data- and
-        weight-gradient GEMMs read it)."""
+        weight-gradient GEMMs read it).  pool: the output feeds a SqueezeExcite -- the same
+        sweep also writes its per-image spatial mean (mdemi_bn_train_fwd_pooled), recorded on
+        the output for squeeze_excite (pooled_of)."""
         _require_cuda(x, weight, bias)
         x = _c(x)
         n = x.shape[0]
@@ -1175,8 +1177,21 @@ class _ChNormFn(torch.autograd.Function):
         mean = torch.empty(nstat, device=x.device, dtype=torch.float32)
         rstd = torch.empty(nstat, device=x.device, dtype=torch.float32)
         lib = L.load()
-        ws = L.workspace(lib.mdemi_chnorm_workspace_size(n, hw, c, groups, int(is_bn)), x.device)
-        if running is not None:
+        pool = bool(pool and running is not None and is_bn and c % 4 == 0 and x.data_ptr() % 16 == 0)
+        ws = L.workspace(lib.mdemi_bn_train_fwd_pooled_workspace_size(n, hw, c) if pool else
+                         lib.mdemi_chnorm_workspace_size(n, hw, c, groups, int(is_bn)), x.device)
+        if pool:
+            rm, rv, tracked, momentum = running
+            pooled = torch.empty(n, c, device=x.device, dtype=torch.float32)
+            L.check(lib.mdemi_bn_train_fwd_pooled(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
+                                                  L.ptr(y16), pooled.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                                  rm.data_ptr(), rv.data_ptr(), L.ptr(tracked), float(momentum), n,
+                                                  hw, c, float(eps), act, ws.data_ptr(), L.stream()),
+                    "bn_train_fwd_pooled")
+            if y16 is not None:
+                set_b16(y, y16)
+            y._mdemi_pooled = (pooled, y._version)
+        elif running is not None:
             rm, rv, tracked, momentum = running
             L.check(lib.mdemi_bn_train_fwd16(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(),
                                              L.ptr(y16), mean.data_ptr(), rstd.data_ptr(), rm.data_ptr(), rv.data_ptr(),
@@ -1197,7 +1212,7 @@ class _ChNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dm, _dr):
         if dy is None:
-            return None, None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, None, None
         x, weight, bias, mean, rstd = ctx.saved_tensors
         groups, is_bn, act = ctx.cfg
         dy = _c(dy)
@@ -1216,15 +1231,26 @@ class _ChNormFn(torch.autograd.Function):
                 "chnorm_bwd")
         if dx16 is not None:
             set_b16(dx, dx16)
-        return dx, dg, db, None, None, None, None, None, None
+        return dx, dg, db, None, None, None, None, None, None, None
 
 
-def batch_norm_nhwc(x, weight, bias, eps=1e-5, act=L.ACT_NONE, running=None, out_b16=False):
+def batch_norm_nhwc(x, weight, bias, eps=1e-5, act=L.ACT_NONE, running=None, out_b16=False, pool=False):
     """Training-mode BatchNorm2d over an NHWC map; returns (y, batch_mean, batch_rstd).
     running=(running_mean, running_var, num_batches_tracked or None, momentum) also applies
     nn.BatchNorm2d's running-statistics update in the same call.  out_b16: y feeds a bf16
-    GEMM (bf16 storage: its bf16 copy is written by the same sweep)."""
-    return _ChNormFn.apply(x, weight, bias, x.shape[-1], True, eps, act, running, out_b16)
+    GEMM (bf16 storage: its bf16 copy is written by the same sweep).  pool: y feeds a
+    SqueezeExcite; with running statistics the same sweep records y's per-image spatial mean
+    for it (pooled_of)."""
+    return _ChNormFn.apply(x, weight, bias, x.shape[-1], True, eps, act, running, out_b16, pool)
+
+
+def pooled_of(x):
+    """The per-image spatial mean [N, C] a BatchNorm sweep recorded on its output x (pool=True),
+    if x is unchanged since; else None."""
+    rec = x.__dict__.get("_mdemi_pooled")
+    if rec is None or rec[1] != x._version or rec[0].shape != (x.shape[0], x.shape[-1]):
+        return None
+    return rec[0]
 
 
 def group_norm_nhwc(x, weight, bias, groups, eps=1e-5, act=L.ACT_NONE):
@@ -1568,7 +1594,9 @@ class _SqueezeExciteFn(torch.autograd.Function):
         n, c = x.shape[0], x.shape[-1]
         hw = x[0].numel() // c
         r = wr.shape[0]
-        pooled = spatial_reduce(x, None, 1.0 / hw)
+        pooled = pooled_of(x)  # recorded by the BatchNorm sweep that produced x, if it pooled
+        if pooled is None:
+            pooled = spatial_reduce(x, None, 1.0 / hw)
         hid = torch.empty(n, r, device=x.device, dtype=torch.float32)
         gate = torch.empty(n, c, device=x.device, dtype=torch.float32)
         L.call("mdemi_se_gate_fwd", pooled.data_ptr(), _c(wr).data_ptr(), br.data_ptr(), _c(we).data_ptr(),
@@ -1592,10 +1620,10 @@ class _SqueezeExciteFn(torch.autograd.Function):
         ws = _ws(lib.mdemi_se_gate_bwd_workspace_size(n, c, r), x.device, slot=3)
         L.check(lib.mdemi_se_gate_bwd(pooled.data_ptr(), _c(wr).data_ptr(), _c(we).data_ptr(), hid.data_ptr(),
                                       gate.data_ptr(), dgate.data_ptr(), dpooled.data_ptr(), dwr.data_ptr(),
-                                      dbr.data_ptr(), dwe.data_ptr(), dbe.data_ptr(), n, c, r, ws.data_ptr(),
-                                      L.stream()), "se_gate_bwd")
-        # d/dx of x * gate plus the pooling path: dpooled / HW broadcast over positions
-        dx = _chan_scale(dy, gate, _scale(dpooled, 1.0 / hw))
+                                      dbr.data_ptr(), dwe.data_ptr(), dbe.data_ptr(), n, c, r, 1.0 / hw,
+                                      ws.data_ptr(), L.stream()), "se_gate_bwd")
+        # d/dx of x * gate plus the pooling path: dpooled / HW (scaled by se_gate_bwd) broadcast
+        dx = _chan_scale(dy, gate, dpooled)
         return dx, dwr, dbr, dwe, dbe
 
 

@@ -54,9 +54,11 @@ def bn_forward(bn: nn.BatchNorm2d, x, act=L.ACT_NONE):
         if bn.track_running_stats and bn.momentum is not None:  # statistics + running update, one call
             # _mdemi_out_b16 (set by the model where the BN's output feeds a conv): under bf16
             # storage the same sweep writes the output's bf16 copy for that GEMM
+            # _mdemi_pool (set where the output feeds a SqueezeExcite): the sweep also pools it
             y, _, _ = mf.batch_norm_nhwc(x, bn.weight, bn.bias, bn.eps, act,
                                          running=(bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                                                  bn.momentum), out_b16=getattr(bn, "_mdemi_out_b16", False))
+                                                  bn.momentum), out_b16=getattr(bn, "_mdemi_out_b16", False),
+                                         pool=getattr(bn, "_mdemi_pool", False))
             return y
         y, mean, rstd = mf.batch_norm_nhwc(x, bn.weight, bn.bias, bn.eps, act)
         if bn.track_running_stats:  # cumulative average (momentum None): needs the count on the host

@@ -116,6 +116,7 @@ class DepthwiseSeparableConv(nn.Module):
         self.has_residual = stride == 1 and in_chs == out_chs
         self.conv_dw = Conv2dSame(in_chs, in_chs, k, stride=stride, groups=in_chs)
         self.bn1 = BatchNormAct2d(in_chs)
+        self.bn1._mdemi_pool = True  # its output feeds the SE: the BN sweep also pools it
         self.act1 = Swish()
         self.se = SqueezeExcite(in_chs, in_chs)
         self.conv_pw = Conv2dSame(in_chs, out_chs, 1)
@@ -140,6 +141,7 @@ class InvertedResidual(nn.Module):
         self.act1 = Swish()
         self.conv_dw = Conv2dSame(mid, mid, k, stride=stride, groups=mid)
         self.bn2 = BatchNormAct2d(mid)
+        self.bn2._mdemi_pool = True  # its output feeds the SE: the BN sweep also pools it
         self.act2 = Swish()
         self.se = SqueezeExcite(mid, in_chs)
         self.conv_pwl = Conv2dSame(mid, out_chs, 1)

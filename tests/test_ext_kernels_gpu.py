@@ -300,6 +300,31 @@ def test_channel_norm_silu(mf):
     close(bg.grad, br.grad, rtol=1e-4)
 
 
+@pytest.mark.parametrize("n,c,h,w", [(2, 16, 5, 7), (3, 240, 30, 41), (8, 1824, 15, 20), (2, 48, 1, 1)])
+def test_bn_train_pooled_for_squeeze_excite(mf, n, c, h, w):
+    """mdemi_bn_train_fwd_pooled (BatchNormAct2d -> SqueezeExcite in the EfficientNet blocks):
+    y, the statistics and the running update equal the plain training forward's bit for bit, and
+    the per-image spatial mean it records equals y's mean in fp64 (to fp32 summation)."""
+    from mdemi import _lib as L
+    x, g, b = rnd(n, c, h, w, seed=70, scale=2), rnd(c, seed=71), rnd(c, seed=72)
+    xg = nhwc(x).float().to(DEV)
+    outs = []
+    for pool in (False, True):
+        rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+        nb = torch.zeros((), dtype=torch.int64, device=DEV)
+        y, mean, rstd = mf.batch_norm_nhwc(xg, g.float().to(DEV), b.float().to(DEV), 1e-3, L.ACT_SILU,
+                                           running=(rm, rv, nb, 0.1), pool=pool)
+        outs.append((y, mean, rstd, rm, rv, nb, mf.pooled_of(y)))
+    (y0, m0, r0, rm0, rv0, nb0, p0), (y1, m1, r1, rm1, rv1, nb1, p1) = outs
+    assert p0 is None and p1 is not None
+    for a, b_ in ((y0, y1), (m0, m1), (r0, r1), (rm0, rm1), (rv0, rv1), (nb0, nb1)):
+        assert torch.equal(a, b_)
+    ref = y1.double().mean(dim=(1, 2))
+    close(p1, ref, rtol=1e-6, atol=1e-7)
+    y1.add_(1.0)  # an in-place change invalidates the recorded mean
+    assert mf.pooled_of(y1) is None
+
+
 @pytest.mark.parametrize("act", ["silu", "relu"])
 def test_mlp_act(mf, act):
     from mdemi import _lib as L
