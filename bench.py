@@ -348,24 +348,35 @@ class _HbmTimers:
                 return per_token * d.heads * d.head_dim * d.B * d.H * d.W
             return f
 
+        def wa_mfma(n_mfma):  # v_mfma_f32_32x32x2_f32 issued per (window, head): 4096 FLOP each
+            def f(args):
+                d = args[0]._obj
+                nwin = d.B * -(-d.H // d.window) * -(-d.W // d.window)
+                return 4096.0 * n_mfma * nwin * d.heads
+            return f
+
         self.specs = {"mdemi_binhead_nhwc_fwd": ("binhead_nhwc_fwd", lambda a: 4.0 * a[4] * a[5] * (a[6] + 3)),
                       "mdemi_binhead_nhwc_bwd": ("binhead_nhwc_bwd", lambda a: 4.0 * a[7] * a[8] * (2 * a[9] + 4)),
                       "mdemi_winattn_fwd": ("winattn_fwd", wa_bytes(16.0)),
                       "mdemi_winattn_bwd_bias": ("winattn_bwd", wa_bytes(32.0))}
+        # window attention is bound by its fp32 MFMA work, not by bytes: 49 tokens padded to 64,
+        # 120 (forward) / 284 (backward) v_mfma_f32_32x32x2_f32 per (window, head) in the
+        # kernels' instruction streams (winattn.hip; counted from the gfx950 ISA)
+        self.mfma = {"winattn_fwd": wa_mfma(120), "winattn_bwd": wa_mfma(284)}
         self.lib = lib
         self.orig = {entry: getattr(lib, entry) for entry in self.specs}
         self.recs = {name: [] for name, _ in self.specs.values()}
         for entry, (name, nbytes) in self.specs.items():
-            setattr(lib, entry, self._wrap(self.orig[entry], nbytes, self.recs[name]))
+            setattr(lib, entry, self._wrap(self.orig[entry], nbytes, self.mfma.get(name), self.recs[name]))
 
     @staticmethod
-    def _wrap(fn, nbytes, recs):
+    def _wrap(fn, nbytes, nflops, recs):
         def timed(*args):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(torch.cuda.current_stream())
             rc = fn(*args)
             e.record(torch.cuda.current_stream())
-            recs.append((nbytes(args), s, e))
+            recs.append((nbytes(args), nflops(args) if nflops else 0.0, s, e))
             return rc
         return timed
 
@@ -378,12 +389,17 @@ class _HbmTimers:
         for name, recs in self.recs.items():
             if not recs:
                 continue
-            t = sum(s.elapsed_time(e) for _, s, e in recs) * 1e-3
-            by = sum(b for b, _, _ in recs)
+            t = sum(s.elapsed_time(e) for _, _, s, e in recs) * 1e-3
+            by = sum(b for b, _, _, _ in recs)
+            fl = sum(f for _, f, _, _ in recs)
             out[name] = {"launches": len(recs), "avg_us": round(t / len(recs) * 1e6, 1),
                          "algorithmic_bytes_per_launch": round(by / len(recs)),
                          "achieved_GBps": round(by / t / 1e9, 1),
                          "frac_of_hbm_peak": round(by / t / 1e9 / HBM_PEAK_GBS, 4)}
+            if fl:
+                out[name].update({"bound": "mfma", "mfma_flops_per_launch": round(fl / len(recs)),
+                                  "mfma_tflops": round(fl / t / 1e12, 2),
+                                  "frac_of_fp32_mfma_peak": round(fl / t / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)})
         return out or None
 
 
@@ -613,6 +629,8 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
     from mdemi.train import build_from_config
     opt = copy.deepcopy(opt)
     opt["dataloader"]["batch_size"] = B
+    torch.cuda.synchronize(device)  # initialises the device context the peak counter needs
+    torch.cuda.reset_peak_memory_stats(device)
     torch.manual_seed(0)
     trainer = build_from_config(opt, device=device, world=world, precision=precision, graph=graph,
                                 ddp=(True if getattr(args, "ddp", False) else None))
@@ -640,7 +658,9 @@ def measure(args, opt, key, H, W, B, rank, world, device, with_roofline, precisi
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     res = {"elapsed": elapsed, "ms": elapsed / args.steps * 1e3, "images": B * na * world * args.steps,
-           "loss": float(loss.item()), "num_accum": na, "trainer": trainer}
+           "loss": float(loss.item()), "num_accum": na, "trainer": trainer,
+           # peak device memory of the build + warm-up + timed steps (bf16 storage: incl. the copies)
+           "peak_mem_GB": round(torch.cuda.max_memory_allocated(device) / 1e9, 2)}
     if trainer.ddp is not None:  # isolated cost of the whole gradient exchange (no overlap): an upper bound on exposed comm
         ddp = trainer.ddp
         torch.cuda.synchronize()
@@ -729,7 +749,7 @@ def measure_secondary(args, sk, rank, world, device):
     out = {"workload": wk["workload"], "reference_config": wk["ref_cfg"], "per_gpu_batch": B,
            "image": [wk["h"], wk["w"]], "matmul_precision": prec, "hipgraph": graph, "steps": sub.steps,
            "images_per_sec": round(sec["images"] / sec["elapsed"], 3), "ms_per_step": round(sec["ms"], 2),
-           "loss": round(sec["loss"], 5), "cpu_baseline": cpu}
+           "loss": round(sec["loss"], 5), "peak_mem_GB": sec["peak_mem_GB"], "cpu_baseline": cpu}
     if "roofline" in sec:
         out["roofline"] = sec["roofline"]
         out["step_mfma_frac"] = sec["extra"]["step_mfma_frac"]
@@ -940,6 +960,7 @@ def main():
                        "parallelism": f"dp{world}", "reference_config": ref_cfg,
                        "matmul_precision": precision, "hipgraph": graph},
             "roofline": res.get("roofline"), "cpu_baseline": cpu, "loss": round(res["loss"], 5),
+            "peak_mem_GB": res["peak_mem_GB"],
             "rccl_world": world if (world > 1 or args.ddp) else None,
         }
         if "allreduce" in res:

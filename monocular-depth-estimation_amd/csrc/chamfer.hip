@@ -129,7 +129,25 @@ __global__ void __launch_bounds__(CH_NT) chamfer_final(const float* __restrict__
   for (int i = tid; i < P; i += CH_NT) {
     float best = INFINITY, bt = 0.f;
     double cnt = 0.0, sum = 0.0;
-    for (int c = 0; c < nchunk; ++c) {
+    // the chunks in order, U at a time with all their loads issued first (one round trip per
+    // U chunks instead of one per chunk: 178 -> ~30 us at 300 chunks x 8 images)
+    constexpr int U = 8;
+    int c = 0;
+    for (; c + U <= nchunk; c += U) {
+      float m[U], t[U], cn[U], su[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t o = ((int64_t)b * nchunk + c + u) * P + i;
+        m[u] = pmin[o]; t[u] = pt[o]; cn[u] = pcnt[o]; su[u] = psum[o];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (m[u] < best) { best = m[u]; bt = t[u]; }
+        cnt += cn[u];
+        sum += su[u];
+      }
+    }
+    for (; c < nchunk; ++c) {
       const int64_t o = ((int64_t)b * nchunk + c) * P + i;
       const float m = pmin[o];
       if (m < best) { best = m; bt = pt[o]; }

@@ -97,16 +97,17 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const fl
 //   6: 256-row tile (waves of 128x64), BK32, 1 buffer   7: 256-row tile, BK16, 2 buffers
 //   (a BK64 single-buffer variant measured no faster than 4 on the model's shapes:
 //   profiles/round3/gemm_study_bk64.txt)
-//   8..11: direct-to-LDS staging (buffer_load ... lds, gemm_glds_kernel.h), dense 16-B
+//   8..12: direct-to-LDS staging (buffer_load ... lds, gemm_glds_kernel.h), dense 16-B
 //   operands without a load-time op only: 8 128-row BK32, 9 256-row BK16, 10 256-row
-//   BK32 (96 KiB, one workgroup per CU), 11 128-row BK16
+//   BK32 (96 KiB, one workgroup per CU), 11 128-row BK16, 12 128-row x 192-column BK32 (the
+//   N = 192 / 576 shapes of the Swin stage 0: no half-empty 128-column tile)
 // No variant wins every shape (e.g. weight-gradient GEMMs over few output
 // tiles want BK32/2 buffers, token-major forwards want BK32/1 buffer), so by
 // default each distinct (layouts, ops, M, N, K, batch, split) is timed once
 // over the candidates on first use and the winner cached.  All variants add
 // the k products in the same order and split K at the same 32-element
 // boundaries, so the choice never changes a result bit.
-constexpr int NVARIANTS = 12;
+constexpr int NVARIANTS = 13;
 static int g_variant = -1;  // -1: autotune per shape
 // A/B switches (environment, read once): MDEMI_GEMM_TAIL_SPLIT=0 disables the tail split,
 // MDEMI_GEMM_INLINE_REDUCE=0 combines split-K slabs with the separate reduce kernel.
@@ -116,6 +117,16 @@ static bool env_on(const char* name) {
 }
 static bool g_tail_split = env_on("MDEMI_GEMM_TAIL_SPLIT");
 static bool g_inline_reduce = env_on("MDEMI_GEMM_INLINE_REDUCE");
+// The bf16 families combine their split-K slabs with the separate reduce kernel by default: its split GEMMs are the small-grid EfficientNet / decoder weight gradients, where
+// one last-arriving workgroup reading every other slab serialises on its fetch rate
+// (~32 GB/s per workgroup: profiles/round6/) -- configs[4] 145.3 -> 151.0 img/s on one box
+// (profiles/round6/ab_inline_reduce.txt).  MDEMI_GEMM_INLINE_REDUCE_B16=1 restores the
+// in-kernel combine.
+static bool env_set(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] && v[0] != '0';
+}
+static bool g_inline_reduce_b16 = env_set("MDEMI_GEMM_INLINE_REDUCE_B16");
 static int g_variant_m16 = -1;  // 16-bit family (bf16 / split fp32): 0 two LDS buffers, 1 one
 static int g_variant_b16 = -1;  // bf16-operand family: 0 128-row tile, 1 256-row tile, 2 128-row x 2 K tiles
 static int g_group_m = 8;
@@ -142,9 +153,10 @@ static KernelFn pick_kernel(int al, int bl, int aop, int bop, int v) {
 
 static int variant_bk(int v, int mode) {
   if (mode != GEMM_F32) return 32;  // the 16-bit and bf16-operand families: BK 32
-  if (v >= 8) return (v == 8 || v == 10) ? 32 : 16;
+  if (v >= 8) return (v == 8 || v == 10 || v == 12) ? 32 : 16;
   return (v >= 3 && v != 7) ? 32 : 16;
 }
+static int variant_cols(int v, int mode) { return (mode == GEMM_F32 && v == 12) ? 192 : GBN; }
 static int variant_rows(int v, int mode) {
   if (mode == GEMM_B16) return v == 1 ? 2 * GBM : GBM;
   return (mode != GEMM_F32 ? (v == 2 || v == 4) : (v == 6 || v == 7 || v == 9 || v == 10)) ? 2 * GBM : GBM;
@@ -287,7 +299,7 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
   const int vrows = variant_rows(variant, mode);  // 256-row variants: 16-bit 2, fp32 6 and 7
   p.tiles_m1 = p.m_split / vrows;
   p.tiles_m = (int)cdiv(d->M - p.m_split, vrows);
-  p.tiles_n = (int)cdiv(d->N, GBN);
+  p.tiles_n = (int)cdiv(d->N, variant_cols(variant, mode));
   p.group_m = g_group_m;
 }
 
@@ -382,7 +394,10 @@ static int launch(const mdemi_gemm_desc* d, int variant, hipStream_t st, int mod
   const int64_t nblocks = (int64_t)p.tiles_m1 * p.tiles_n + (int64_t)p.tiles_m * p.tiles_n * d->batch * p.split;
   MDEMI_REQUIRE(nblocks < (int64_t)1 << 31, "gemm: grid too large");
   const bool deep = p.split > 1 && colsum_combine(d, p) && !p.c16;  // the column-sum combine writes fp32 only
-  if (p.split > 1 && !deep && (g_inline_reduce || p.m_split > 0)) {
+  // both bf16 families (bf16 operands in HBM, or rounded at staging) combine alike, so the
+  // bf16-storage step stays bit-identical to the fp32-operand bf16 step
+  const bool inline_reduce = (mode == GEMM_B16 || mode == GEMM_BF16) ? g_inline_reduce_b16 : g_inline_reduce;
+  if (p.split > 1 && !deep && (inline_reduce || p.m_split > 0)) {
     p.tile_cnt = tile_counters((int64_t)p.tiles_m * p.tiles_n * d->batch, st);
     if (p.tile_cnt && rowsum_part) p.rowsum_out = d->rowsum_a;  // the last arrivers sum the row partials
   }
@@ -441,10 +456,10 @@ static int choose_variant(const mdemi_gemm_desc* d, hipStream_t st, int mode, co
   }
   if (!tunable(d, st)) return 0;
   if (ext && ext->c16 && (ext->c16 == ext->a16 || ext->c16 == ext->b16)) return 0;
-  static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+  static const int cands_f32[] = {0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12};
   static const int cands_m16[] = {0, 1, 2, 3, 4};
   const int* cands = mode != GEMM_F32 ? cands_m16 : cands_f32;
-  int ncand = mode == GEMM_BF16 ? 5 : mode == GEMM_F32E ? 3 : mode == GEMM_B16 ? 3 : 11;
+  int ncand = mode == GEMM_BF16 ? 5 : mode == GEMM_F32E ? 3 : mode == GEMM_B16 ? 3 : 12;
   if (mode == GEMM_F32) {
     GemmParams q;
     fill_params(d, q, 0, mode);

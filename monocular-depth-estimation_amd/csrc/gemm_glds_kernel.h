@@ -47,11 +47,12 @@ struct GSwz {  // chunk permutation of a [row][k] image
   __device__ static int of(int row) { return BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3; }
 };
 
-// k-contiguous operand, one 128-row [row][BK] image.  Wave w issues instructions
-// q = w * NI + i (i < NI), each covering rows RPI*q .. RPI*q + RPI-1.
-template <int BK>
+// k-contiguous operand, one ROWS-row (128, or 192 for the B operand of the 192-column tile)
+// [row][BK] image.  Wave w issues instructions q = w * NI + i (i < NI), each covering rows
+// RPI*q .. RPI*q + RPI-1.
+template <int BK, int ROWS = 128>
 struct GLoadKC {
-  static constexpr int CH = BK / 4, RPI = 64 / CH, NI = 128 / RPI / 4;
+  static constexpr int CH = BK / 4, RPI = 64 / CH, NI = ROWS / RPI / 4;
   const float* base; int K;
   int voff[NI];  // byte offset of this lane's (row, chunk) within the tile, k0 = 0 (BUF_OOB: row out of range)
   int kch[NI];   // this lane's k chunk (the global chunk stored at its LDS slot)
@@ -106,20 +107,55 @@ struct GLoadMN {
   }
 };
 
-template <int L, int BK>
-using GLoad = typename std::conditional<L == MDEMI_L_KCONTIG, GLoadKC<BK>, GLoadMN<BK>>::type;
+// m/n-contiguous operand, columns 128 .. 191 of the 192-column tile: one [BK][64] image.
+// Instruction q covers k rows 4q .. 4q+3 (lane j -> k row 4q + j/16, columns 4 (j%16) ..).
+template <int BK>
+struct GLoadMN64 {
+  static constexpr int NI = BK / 4 / 4;
+  const float* base; int64_t ld; int K;
+  int voff, kl;
+  __device__ void init(const float* p, int64_t ld_, int cols, int K_, int c0, int wid, int lane) {
+    base = p + c0; ld = ld_; K = K_;
+    const int col = 4 * (lane & 15);
+    kl = 4 * (wid * NI) + (lane >> 4);
+    voff = c0 + col < cols ? (int)(((int64_t)kl * ld + col) * 4) : BUF_OOB;
+  }
+  __device__ void issue(int k0, float* img, int wid) const {
+    const auto rs = make_rsrc(base + (int64_t)k0 * ld);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = wid * NI + i;
+      const bool kin = k0 + kl + 4 * i < K;
+      glds16(rs, img + q * 256, kin && voff != BUF_OOB ? voff + (int)(4 * i * ld * 4) : BUF_OOB);
+    }
+  }
+};
+
+// 4 consecutive k (8g + 4h ..) of column c of a [BK][pitch] image (pitch 128 or 64)
+__device__ __forceinline__ float4 mn_frag_pitch(const float* img, int pitch, int c, int g, int h) {
+  const float* p = img + (8 * g + 4 * h) * pitch + c;
+  return make_float4(p[0], p[pitch], p[2 * pitch], p[3 * pitch]);
+}
+
+template <int L, int BK, int ROWS = 128>
+using GLoad = typename std::conditional<L == MDEMI_L_KCONTIG, GLoadKC<BK, ROWS>, GLoadMN<BK>>::type;
 
 // BMT: block-tile rows (128: 2x2 waves of 64x64; 256: 2x2 waves of 128x64, A as two
-// 128-row images).  BK: 16 or 32.  OCC: waves per SIMD the register budget targets.
-template <int AL, int BL, int BMT, int BK, int OCC>
+// 128-row images).  BNT: block-tile columns, 128, or 192 (2x2 waves of 64x96: the N = 192 /
+// 576 GEMMs of the Swin stage 0, which a 128-column tile covers in 1.5 / 4.5 tiles; B as one
+// 192-row k-contiguous image, or a 128- and a 64-column m/n-contiguous image).  BK: 16 or
+// 32.  OCC: waves per SIMD the register budget targets.
+template <int AL, int BL, int BMT, int BK, int OCC, int BNT = 128>
 __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void gemm_glds_kernel(
     GemmParams p) {
   static_assert(AL != MDEMI_L_CONV && BL != MDEMI_L_CONV, "dense operands only");
   static_assert(BK == 16 || BK == 32, "BK");
+  static_assert(BNT == 128 || (BNT == 192 && BMT == 128), "192-column tiles: 128 rows");
   constexpr int NA = BMT / 128, IM = BMT / 64, WTM = BMT / 2;
-  constexpr int IMG = 128 * BK;          // floats per 128-row (or 128-column) image
-  constexpr int STAGE = (NA + 1) * IMG;  // A images + the B image
-  constexpr int NG = BK / 8;             // k groups per tile
+  constexpr int WTN = BNT / 2, IN = WTN / 32;  // wave tile columns, 32-column accumulators
+  constexpr int IMG = 128 * BK;               // floats per 128-row (or 128-column) image
+  constexpr int STAGE = NA * IMG + BNT * BK;  // A images + the B image(s)
+  constexpr int NG = BK / 8;                  // k groups per tile
   // stage 0 is `smem` (the epilogue's split-K hand-off flag and the row-sum reduction reuse
   // it after the loop), stage 1 `smem1`
   __shared__ __attribute__((aligned(16))) float smem[STAGE];
@@ -130,26 +166,29 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   const int wm = wid >> 1, wn = wid & 1;
   const GemmJob job = job_of(p);
   const int b = job.b, sidx = job.sidx, tm = job.tm, tn = job.tn;
-  const int bm = tm * BMT, bn = tn * GBN;
+  const int bm = tm * BMT, bn = tn * BNT;
 
   using LA = GLoad<AL, BK>;
-  using LB = GLoad<BL, BK>;
+  using LB = GLoad<BL, BK, BNT>;
+  constexpr bool B64 = BNT == 192 && BL == MDEMI_L_MNCONTIG;  // the extra 64-column B image
   LA la[NA];
   LB lb;
+  GLoadMN64<BK> lb64;
 #pragma unroll
   for (int a = 0; a < NA; ++a)
     la[a].init(p.A + boff(p, b, p.a_bs, p.a_bs2), p.lda, p.M, p.K, bm + 128 * a, wid, lane);
   lb.init(p.B + boff(p, b, p.b_bs, p.b_bs2), p.ldb, p.N, p.K, bn, wid, lane);
+  if constexpr (B64) lb64.init(p.B + boff(p, b, p.b_bs, p.b_bs2), p.ldb, p.N, p.K, bn + 128, wid, lane);
 
   const int ktiles_total = (p.K + BK - 1) / BK;
   const int kt_begin = job.split ? sidx * p.ktile_per_split : 0;
   const int kt_end = job.split ? min(ktiles_total, kt_begin + p.ktile_per_split) : ktiles_total;
 
-  floatx16 acc[IM][2];
+  floatx16 acc[IM][IN];
 #pragma unroll
   for (int a = 0; a < IM; ++a)
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < IN; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
 
@@ -157,6 +196,7 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 #pragma unroll
     for (int a = 0; a < NA; ++a) la[a].issue(kt * BK, st + a * IMG, wid);
     lb.issue(kt * BK, st + NA * IMG, wid);
+    if constexpr (B64) lb64.issue(kt * BK, st + NA * IMG + IMG, wid);
   };
 
   // bias-gradient row sums of an m-contiguous A, in the register kernel's order
@@ -171,7 +211,17 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
 #pragma unroll
   for (int i = 0; i < IM; ++i) rA[i] = (wm * WTM + 32 * i + l31) & 127;
   const int aimg = (wm * WTM) >> 7;
-  const int rb0 = wn * 64 + l31, rb1 = rb0 + 32;
+  // B fragment j: columns cb_j = wn * WTN + 32 j (+ l31); for the 192-column m/n-contiguous
+  // tile, those >= 128 come from the 64-column image (a wave-uniform choice)
+  auto fragB = [&](const float* b_s, int j, int g) -> float4 {
+    const int cb = wn * WTN + 32 * j;
+    if constexpr (B64) {
+      if (cb >= 128) return mn_frag_pitch(b_s + IMG, 64, cb - 128 + l31, g, h);
+      return mn_frag_pitch(b_s, 128, cb + l31, g, h);
+    } else {
+      return LB::frag(b_s, cb + l31, g, h);
+    }
+  };
 
   // One K tile: issue the DMA of tile kt+1 into `nxt`, then the row sums and MFMAs of tile
   // kt from `cur`.  The two stages are separate __shared__ objects and every call below
@@ -192,28 +242,27 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
     }
     const float* a_s = cur + aimg * IMG;
     const float* b_s = cur + NA * IMG;
-    float4 fa[2][IM], fb[2][2];
+    float4 fa[2][IM], fb[2][IN];
 #pragma unroll
     for (int i = 0; i < IM; ++i) fa[0][i] = LA::frag(a_s, rA[i], 0, h);
-    fb[0][0] = LB::frag(b_s, rb0, 0, h);
-    fb[0][1] = LB::frag(b_s, rb1, 0, h);
+#pragma unroll
+    for (int j = 0; j < IN; ++j) fb[0][j] = fragB(b_s, j, 0);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int c = g & 1, n = c ^ 1;
       if (g + 1 < NG) {
 #pragma unroll
         for (int i = 0; i < IM; ++i) fa[n][i] = LA::frag(a_s, rA[i], g + 1, h);
-        fb[n][0] = LB::frag(b_s, rb0, g + 1, h);
-        fb[n][1] = LB::frag(b_s, rb1, g + 1, h);
+#pragma unroll
+        for (int j = 0; j < IN; ++j) fb[n][j] = fragB(b_s, j, g + 1);
       }
       // keep the reads of group g+1 ahead of group g's MFMAs (the scheduler would otherwise
       // sink them behind the MFMAs and expose their latency at the next group)
       __builtin_amdgcn_sched_barrier(0);
 #define MDEMI_GSTEP(X)                                                                             \
-  _Pragma("unroll") for (int i = 0; i < IM; ++i) {                                                 \
-    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[c][i].X, fb[c][0].X, acc[i][0], 0, 0, 0);  \
-    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[c][i].X, fb[c][1].X, acc[i][1], 0, 0, 0);  \
-  }
+  _Pragma("unroll") for (int i = 0; i < IM; ++i)                                                   \
+  _Pragma("unroll") for (int j = 0; j < IN; ++j)                                                   \
+    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[c][i].X, fb[c][j].X, acc[i][j], 0, 0, 0);
       MDEMI_GSTEP(x) MDEMI_GSTEP(y) MDEMI_GSTEP(z) MDEMI_GSTEP(w)
 #undef MDEMI_GSTEP
     }
@@ -247,11 +296,13 @@ __global__ __launch_bounds__(GTHREADS) __attribute__((amdgpu_waves_per_eu(OCC, 8
   }
 
 #define EP_IM IM
+#define EP_IN IN
 #define EP_WTM WTM
+#define EP_WTN WTN
 #include "gemm_epilogue.inc"
 }
 
-// variants 8..11 (gemm_f32.hip pick_kernel), instantiated per layout pair in gemm_glds_inst*.hip
+// variants 8..12 (gemm_f32.hip pick_kernel), instantiated per layout pair in gemm_glds_inst*.hip
 template <int AL, int BL>
 static void (*pick_glds(int v))(GemmParams) {
   if constexpr (AL == MDEMI_L_CONV || BL == MDEMI_L_CONV) {
@@ -262,6 +313,7 @@ static void (*pick_glds(int v))(GemmParams) {
       case 9: return gemm_glds_kernel<AL, BL, 256, 16, 2>;
       case 10: return gemm_glds_kernel<AL, BL, 256, 32, 1>;
       case 11: return gemm_glds_kernel<AL, BL, 128, 16, 3>;
+      case 12: return gemm_glds_kernel<AL, BL, 128, 32, 2, 192>;
       default: return nullptr;
     }
   }

@@ -79,7 +79,7 @@ def _split_fill(tiles, smax, s_legacy):
     unit of work: rounds / split, times 1 % per split for the slab traffic and the last
     arriver's serial combine (tools/gemm_split_study.py, profiles/round5/split_study.txt).  The
     round-4 rule's factor stays unless this one is >= 5 % cheaper by the model."""
-    cus = 256
+    cus = _device_cus()
 
     def cost(s):
         return -(-tiles * s // cus) / s * (1.0 + 0.01 * s)
@@ -89,6 +89,17 @@ def _split_fill(tiles, smax, s_legacy):
 
 
 _SPLIT_MIN_KTILES = int(os.environ.get("MDEMI_SPLIT_MIN_KTILES", "16"))  # bf16; K tiles of 16 rows
+_CUS = [int(os.environ.get("MDEMI_CUS", "0"))]  # > 0: override the compute-unit count (A/B runs)
+
+
+def _device_cus():
+    """Compute units of the current device (the split model's round size), read once."""
+    if _CUS[0] <= 0:
+        try:
+            _CUS[0] = int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+        except (RuntimeError, AssertionError):
+            _CUS[0] = 256  # MI355X; only reached without a GPU (the CPU tests of the split plan)
+    return _CUS[0]
 
 
 def _draw_seed(device):
@@ -174,6 +185,22 @@ def _b16_rec(t, numel):
     return rec[0]
 
 
+_B16_CHECK = os.environ.get("MDEMI_B16_CHECK") == "1"
+
+
+def _b16_checked(t, b):
+    """MDEMI_B16_CHECK=1: every reuse of a recorded bf16 copy is compared with a fresh RNE cast
+    of the fp32 tensor (a raw in-place write that torch's version counter did not see would
+    otherwise hand a stale operand to a bf16 GEMM silently)."""
+    if not _B16_CHECK:
+        return b
+    fresh = torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
+    L.call("mdemi_cast_bf16", t.data_ptr(), fresh.data_ptr(), t.numel(), L.stream())
+    if not torch.equal(fresh.view(torch.int16), b.view(t.shape).view(torch.int16)):
+        raise RuntimeError(f"stale bf16 copy of a {tuple(t.shape)} tensor (MDEMI_B16_CHECK)")
+    return b
+
+
 def b16_of(t, convert=True):
     """The bf16 copy of contiguous fp32 tensor t: the recorded one (set_b16; on t or on the
     tensor t is a whole view of) if still valid, else (convert) a cast sweep, recorded on t --
@@ -181,13 +208,13 @@ def b16_of(t, convert=True):
     (non-contiguous, unaligned)."""
     b = _b16_rec(t, t.numel())
     if b is not None:
-        return b
+        return _b16_checked(t, b)
     base = t._base
     whole = base is not None and base.data_ptr() == t.data_ptr() and base.numel() == t.numel()
     if whole:
         b = _b16_rec(base, t.numel())
         if b is not None:
-            return b.view(t.shape)
+            return _b16_checked(t, b.view(t.shape))
     if not convert or not t.is_contiguous() or t.data_ptr() % 16 or t.dtype != torch.float32:
         return None
     b = torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
@@ -287,6 +314,11 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     if (_PRECISION[0] == "bf16" and _B16_STORAGE[0] and a16 is None and b16 is None and a_op == L.OP_NONE
             and b_op == L.OP_NONE and A is not None and B is not None):
         a16, b16 = _b16_operands(d, A, B, a_off, b_off, rowsum_a, lib)
+        if a16 is not None and rowsum_a is not None and (a_layout != L.L_MNCONTIG or batch != 1):
+            # the column-sum substitution below assumes an m-contiguous [K][M] A of batch 1
+            # (mdemi_gemm_desc.rowsum_a's own contract): anything else keeps the in-kernel
+            # sums on the fp32-operand path
+            a16 = b16 = None
         if a16 is not None and rowsum_a is not None:
             # the bias-gradient row sums of the unrounded fp32 A: a column sum over A's k rows
             # (A m-contiguous [K][M]), instead of the GEMM's in-kernel sums
@@ -567,8 +599,12 @@ class _Conv2dFn(torch.autograd.Function):
         wf = conv_weight_layout(weight, L.WL_OHWI).view(cout, K)
         pointwise = kh == 1 and kw == 1 and stride == 1 and pad == 0
         if pointwise:
+            # bf16: the split-K heuristic too -- the 15x20 / 30x40 EfficientNet projections have
+            # 57-400 output tiles over K up to 3072, and the bf16 families combine slabs with a
+            # parallel reduce kernel (gemm_f32.hip g_inline_reduce_b16)
             gemm(x, wf, out, M, cout, K, lda=c, ldb=K, ldc=cout, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
-                 bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act, split_k=1)
+                 bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act,
+                 split_k=None if _PRECISION[0] == "bf16" else 1)
         else:
             if c % 4:
                 raise ValueError("conv2d: implicit-GEMM path needs C % 4 == 0")

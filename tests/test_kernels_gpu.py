@@ -608,19 +608,20 @@ def test_gemm_variants_bit_identical(mf, layouts):
     """Every pipelining variant (and hence the per-shape autotuner's pick) adds
     the k products in the same order: results must match bit for bit,
     including split-K and a K that is not a multiple of 32 -- the register-staged
-    variants 0..7 and the direct-to-LDS variants 8..11 (gemm_glds_kernel.h) alike, with
-    the bias-gradient row sums of an m-contiguous A (wgrad) too.  A K that is not a
-    multiple of 4 cannot be staged by 16-B DMA: a forced direct-to-LDS variant falls back
-    to the register kernel and still agrees."""
+    variants 0..7 and the direct-to-LDS variants 8..12 (gemm_glds_kernel.h; 12 is the
+    128x192 tile of the N = 192 / 576 stage-0 shapes, here on N = 192 exactly and on ragged
+    N) alike, with the bias-gradient row sums of an m-contiguous A (wgrad) too.  A K that
+    is not a multiple of 4 cannot be staged by 16-B DMA: a forced direct-to-LDS variant
+    falls back to the register kernel and still agrees."""
     from mdemi import _lib as L
     lib = L.load()
-    for M, N, K in ((700, 300, 1000), (520, 264, 999)):
+    for M, N, K in ((700, 300, 1000), (520, 264, 999), (384, 192, 320)):
         a = torch.randn(M, K, device=DEV)
         b = torch.randn(N, K, device=DEV)
         at, bt = a.t().contiguous(), b.t().contiguous()
         outs = []
         try:
-            for v in range(12):
+            for v in range(13):
                 L.check(lib.mdemi_gemm_set_variant(v, 8), "set_variant")
                 for split in (1, 4, 5):
                     c = torch.empty(M, N, device=DEV)
