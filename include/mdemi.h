@@ -176,11 +176,12 @@ int mdemi_gemm_set_variant(int32_t variant, int32_t group_m);
  * tile with two LDS buffers, 1 = one buffer, 2 = 256-row tile; -1 = per-shape
  * autotune (default; all bit-identical). */
 int mdemi_gemm_set_variant_m16(int32_t variant);
-/* scheduling switches (process-global; defaults on, or from MDEMI_GEMM_TAIL_SPLIT /
- * MDEMI_GEMM_INLINE_REDUCE = 0): tail_split -- a whole-K GEMM whose tiles leave a thin
- * last round of workgroups splits the rows of the leftover tiles over K (a plan that
- * depends on the shape only); inline_reduce -- split-K slabs are combined by the
- * last-arriving piece of each tile instead of a separate reduce launch. */
+/* scheduling switches of the fp32 family (process-global; defaults from the environment:
+ * MDEMI_GEMM_TAIL_SPLIT, on unless 0; MDEMI_GEMM_INLINE_REDUCE, off unless 1): tail_split --
+ * a whole-K GEMM whose tiles leave a thin last round of workgroups splits the rows of the
+ * leftover tiles over K (a plan that depends on the shape only); inline_reduce -- split-K
+ * slabs are combined by the last-arriving piece of each tile instead of a separate reduce
+ * launch (bit-identical either way; the bf16 families follow MDEMI_GEMM_INLINE_REDUCE_B16). */
 int mdemi_gemm_set_options(int32_t tail_split, int32_t inline_reduce);
 
 /* column / row sums (bias gradients: db[j] = sum_i dY[i][j])

@@ -109,23 +109,24 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p, const fl
 // boundaries, so the choice never changes a result bit.
 constexpr int NVARIANTS = 13;
 static int g_variant = -1;  // -1: autotune per shape
-// A/B switches (environment, read once): MDEMI_GEMM_TAIL_SPLIT=0 disables the tail split,
-// MDEMI_GEMM_INLINE_REDUCE=0 combines split-K slabs with the separate reduce kernel.
+// A/B switches (environment, read once): MDEMI_GEMM_TAIL_SPLIT=0 disables the tail split;
+// MDEMI_GEMM_INLINE_REDUCE=1 (fp32) / MDEMI_GEMM_INLINE_REDUCE_B16=1 (bf16) combine split-K
+// slabs in the kernel (the tile's last-arriving workgroup) instead of the separate reduce
+// kernel.  The separate, chip-wide reduce is the default since round 6: one last arriver
+// reading every other slab of its tile serialises on a workgroup's fetch rate (~32 GB/s:
+// profiles/round6/b16_variants_*.txt), which the bf16 step's small-grid weight gradients
+// hit hardest -- configs[4] 145.5 -> 152.2 img/s, NYU 60.2 -> 60.8, AdaBins 73.6 -> 73.9 on
+// one box (profiles/round6/ab_inline_reduce.txt).  The tail split always combines inline.
 static bool env_on(const char* name) {
   const char* v = getenv(name);
   return !(v && v[0] == '0');
 }
-static bool g_tail_split = env_on("MDEMI_GEMM_TAIL_SPLIT");
-static bool g_inline_reduce = env_on("MDEMI_GEMM_INLINE_REDUCE");
-// The bf16 families combine their split-K slabs with the separate reduce kernel by default: its split GEMMs are the small-grid EfficientNet / decoder weight gradients, where
-// one last-arriving workgroup reading every other slab serialises on its fetch rate
-// (~32 GB/s per workgroup: profiles/round6/) -- configs[4] 145.3 -> 151.0 img/s on one box
-// (profiles/round6/ab_inline_reduce.txt).  MDEMI_GEMM_INLINE_REDUCE_B16=1 restores the
-// in-kernel combine.
 static bool env_set(const char* name) {
   const char* v = getenv(name);
   return v && v[0] && v[0] != '0';
 }
+static bool g_tail_split = env_on("MDEMI_GEMM_TAIL_SPLIT");
+static bool g_inline_reduce = env_set("MDEMI_GEMM_INLINE_REDUCE");
 static bool g_inline_reduce_b16 = env_set("MDEMI_GEMM_INLINE_REDUCE_B16");
 static int g_variant_m16 = -1;  // 16-bit family (bf16 / split fp32): 0 two LDS buffers, 1 one
 static int g_variant_b16 = -1;  // bf16-operand family: 0 128-row tile, 1 256-row tile, 2 128-row x 2 K tiles

@@ -683,7 +683,7 @@ def test_gemm_tail_split(mf, layouts):
         outs = [(v, run(v, 1)) for v in (0, 1, 3, 4, 5, 6, 7)]
     finally:
         lib.mdemi_gemm_set_variant(-1, 8)
-        lib.mdemi_gemm_set_options(1, 1)
+        lib.mdemi_gemm_set_options(1, 0)  # the defaults: tail split on, separate split-K reduce
     ref = (a.double() @ b.double().t() + bias.double() + res.double()).float()
     close(plain, ref, rtol=1e-5 * math.sqrt(K))
     m_split = _tail_plan_m_split(M, N, K, torch.cuda.get_device_properties(DEV).multi_processor_count)
@@ -746,7 +746,7 @@ def test_gemm_inline_combine_matches_reduce_kernel(mf, layouts):
             k, krs = run(0)
             outs = [run(1) for _ in range(3)]
         finally:
-            lib.mdemi_gemm_set_options(1, 1)
+            lib.mdemi_gemm_set_options(1, 0)  # the defaults: tail split on, separate split-K reduce
         want = a.double() @ b.double().t() + (bias.double() if layouts == "fwd" else 0.0)
         close(k, want.float(), rtol=1e-5 * math.sqrt(K))
         for c, rs in outs:
