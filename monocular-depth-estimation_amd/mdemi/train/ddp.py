@@ -27,7 +27,18 @@ gradients accumulate; the reduction happens on the first backward outside it.
 
 If something replaced a ``.grad`` (``zero_grad(set_to_none=True)``, a first
 step before the views were installed), the hook copies it into the bucket
-slice and re-installs the view, so the protocol stays correct."""
+slice and re-installs the view, so the protocol stays correct.
+
+Bucket rebuild (``rebuild_buckets``, on by default; torch DDP rebuilds its buckets after the
+first iteration for the same reason).  Reverse registration order is only a guess at the
+order backward produces gradients: a parameter registered early but used late (NeW-CRFs'
+backbone out-norms, read by the decoder) finishes its bucket late, and strict index order
+then holds every later bucket back (bench.py --ddp measured bucket 4 of the large07 KITTI
+step ready 8 ms before the end of backward, holding back 9 buckets that were ready 18-62 ms
+earlier).  The first synchronised backward records the order the gradients actually land
+in; ``finish()`` then regroups the parameters in that order (rank 0's order, broadcast, so
+every rank builds the same buckets) and moves the reduced gradients into the new buffers.
+From the second step on, buckets become ready in index order."""
 from __future__ import annotations
 
 import contextlib
@@ -39,8 +50,9 @@ import torch.distributed as dist
 class GradAllReduce:
     SLOT_ALIGN = 64  # elements
 
-    def __init__(self, model, bucket_mb: float = 64.0, group=None):
+    def __init__(self, model, bucket_mb: float = 64.0, group=None, rebuild_buckets: bool = True):
         self.group = group
+        self.bucket_mb = bucket_mb
         # finish() turns the sums into means in place; a consumer that applies 1/world itself
         # (FusedAdamW.grad_scale, wired by Trainer) sets this False and saves that sweep
         self.scale_in_finish = True
@@ -52,11 +64,31 @@ class GradAllReduce:
         dev = self.params[0].device
         if any(p.dtype != dtype or p.device != dev for p in self.params):
             raise ValueError("GradAllReduce: all parameters must share one dtype and device")
+        self._layout(list(reversed(self.params)))
+        self._install_views(copy_existing=True)
+        self._pindex = {p: i for i, p in enumerate(self.params)}
+        self._rebuild = rebuild_buckets
+        self._arrivals: list[int] = []  # parameter indices in gradient-arrival order (first synced backward)
+        self.rebuilt = False
+        self.launch_order: list[int] = []
+        self.last_launch_order: list[int] = []
+        self._works = []
+        self._sync = True
+        # trace_events: record a HIP event on the compute stream when each bucket becomes ready
+        # (its last gradient landed) and when it is launched, and one at the end of backward
+        # (finish) -- bench.py --ddp reports the offsets (eager steps only, never in a capture)
+        self.trace_events = False
+        self.trace = None
+        self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
+        self.reset()
+
+    def _layout(self, order):
+        """Buckets of ~bucket_mb over the parameters in `order`, one zeroed flat buffer each."""
         self.buckets, cur, size = [], [], 0
-        for p in reversed(self.params):
+        for p in order:
             cur.append(p)
             size += p.numel() * p.element_size()
-            if size >= bucket_mb * 2 ** 20:
+            if size >= self.bucket_mb * 2 ** 20:
                 self.buckets.append(cur)
                 cur, size = [], 0
         if cur:
@@ -72,20 +104,30 @@ class GradAllReduce:
                 self.bucket_of[p] = bi
                 self.slot[p] = (off, p.numel())
                 off += -(-p.numel() // self.SLOT_ALIGN) * self.SLOT_ALIGN
-            self.flat.append(torch.zeros(off, dtype=dtype, device=dev))
+            self.flat.append(torch.zeros(off, dtype=self.params[0].dtype, device=self.params[0].device))
         self.bucket_bytes = [f.numel() * f.element_size() for f in self.flat]
-        self._install_views(copy_existing=True)
-        self.launch_order: list[int] = []
-        self.last_launch_order: list[int] = []
-        self._works = []
-        self._sync = True
-        # trace_events: record a HIP event on the compute stream when each bucket becomes ready
-        # (its last gradient landed) and when it is launched, and one at the end of backward
-        # (finish) -- bench.py --ddp reports the offsets (eager steps only, never in a capture)
-        self.trace_events = False
-        self.trace = None
-        self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
-        self.reset()
+
+    def _rebuild_from_arrivals(self):
+        """Regroup the buckets in the recorded arrival order (rank 0's), keeping the gradients."""
+        seen = set(self._arrivals)
+        order = self._arrivals + [i for i in reversed(range(len(self.params))) if i not in seen]
+        self._arrivals = []
+        self._rebuild = False
+        t = torch.tensor(order, dtype=torch.int64, device=self.flat[0].device)
+        if self.world > 1:
+            dist.broadcast(t, 0, group=self.group)
+        order = [int(i) for i in t.tolist()]
+        pos = {pi: k for k, pi in enumerate(order)}
+        done = [max(pos[self._pindex[p]] for p in b) for b in self.buckets]  # when each bucket completed
+        if all(a < b for a, b in zip(done, done[1:])):
+            return  # already ready in index order (the order inside a bucket does not matter)
+        grads = {p: self._view(p) for p in self.params}  # views into the old buffers (kept alive here)
+        self._layout([self.params[i] for i in order])
+        for p in self.params:
+            v = self._view(p)
+            self._copy(grads[p], v)
+            p.grad = v
+        self.rebuilt = True
 
     # ---- gradient storage ----
     def _view(self, p):
@@ -163,6 +205,8 @@ class GradAllReduce:
             p.grad = self._view(p)
         if not self._sync:
             return
+        if self._rebuild:
+            self._arrivals.append(self._pindex[p])
         bi = self.bucket_of[p]
         self._pending[bi] -= 1
         if self._trace is not None and self._pending[bi] == 0:
@@ -200,6 +244,8 @@ class GradAllReduce:
             if not self._is_view(p):
                 p.grad = self._view(p)
         self.last_launch_order = list(self.launch_order)
+        if self._rebuild and self._arrivals and not (self.flat[0].is_cuda and torch.cuda.is_current_stream_capturing()):
+            self._rebuild_from_arrivals()
         self.reset()
 
     def zero_grad(self):

@@ -101,7 +101,8 @@ def test_bucket_readiness_trace(rccl):
     """the traced step (GradAllReduce.trace_events, bench.py --ddp's
     `allreduce.overlap`) records when each bucket became ready and was launched; buckets
     launch in index order, each no earlier than it was ready, the first ones well before the
-    end of backward; the trace is off again afterwards and leaves the step's results alone."""
+    end of backward; after the first step's bucket rebuild they also become ready in index
+    order; the trace is off again afterwards and leaves the step's results alone."""
     import bench
     from mdemi.train import build_from_config
     opt = _dfv8_opt(1)
@@ -129,6 +130,9 @@ def test_bucket_readiness_trace(rccl):
         assert r["launch_before_end_ms"] >= 0.0, r
     assert rows[0]["ready_before_end_ms"] > rows[-1]["ready_before_end_ms"]
     assert ov["model_exposed_ms"] >= 0.0
+    # the first step regrouped the buckets in gradient-arrival order: from then on they become
+    # ready in index order and none is held back by an earlier, later-finishing bucket
+    assert ov["ready_order_is_index_order"] and ov["held_back_buckets"] == [], ov["ready_order"]
     print(f"{n} buckets, ready order {ov['ready_order']}, held back {ov['held_back_buckets']}, "
           f"8-GPU model exposed {ov['model_exposed_ms']} ms")
 

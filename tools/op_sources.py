@@ -43,9 +43,11 @@ def main():
         fn = getattr(lib, name)
         orig[name] = fn
 
-        def wrapped(*args, _fn=fn, _name=name):
+        def wrapped(*args, _fn=fn, _name=name):  # noqa: E306
             stack = [f for f in traceback.extract_stack()[:-1] if "/mdemi/" in f.filename]
-            where = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in stack[-3:][::-1])
+            inner = [f for f in stack if not f.filename.endswith(("_lib.py",))][-2:]
+            outer = [f for f in stack if not f.filename.endswith(("_lib.py", "functional.py"))][-2:]
+            where = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in (inner + outer)[::-1])
             counts[(_name, where)] += 1
             return _fn(*args)
         setattr(lib, name, wrapped)
