@@ -83,6 +83,13 @@ int mdemi_softmax_bwd(const float* y, const float* dy, float* dx, int64_t rows, 
 int mdemi_softmax_fwd16(const float* x, float* y, void* y16, int64_t rows, int32_t cols, float scale, void* stream);
 int mdemi_softmax_bwd16(const float* y, const float* dy, float* dx, void* dx16, int64_t rows, int32_t cols,
                         float scale, int32_t accumulate, void* stream);
+/* Softmax whose bf16 copy y16 (required) is the DROPPED-OUT probabilities: y16 = RNE bf16 of
+ * mdemi_dropout_dev(y, p, seed_dev, seed_add, offset) element for element (the mask index is
+ * the element's flat position in y), while y keeps the softmax itself for the backward.  The
+ * attention dropout of luna_layer.py:213-215,244-246 / self_attention.py:72-74 fused into the
+ * probabilities sweep: P.V reads y16, with no dropout launch and no fp32 copy of dropout(P). */
+int mdemi_softmax_fwd_drop16(const float* x, float* y, void* y16, int64_t rows, int32_t cols, float scale, float p,
+                             const uint64_t* seed_dev, uint64_t seed_add, uint64_t offset, void* stream);
 
 /* y = act(x) elementwise (MDEMI_ACT_* code): the standalone activations of
  * UpscaleConcatAct (layer_utils.py:121) and the bin regressor

@@ -118,6 +118,18 @@ __device__ __forceinline__ float aux_grad(int act, float a) {
   }
 }
 
+// Inverted dropout's keep test: element ctr kept when uniform01(seed, ctr) >= p, u from a
+// splitmix64 finalizer of (seed, ctr) -- one definition for the dropout sweeps (heads.hip),
+// the GEMM epilogue's fused dropout and the softmax sweep's dropped bf16 copy, so every
+// form of the mask agrees bit for bit.
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t ctr) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(uint32_t)(z >> 40) * (1.f / 16777216.f);
+}
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Deterministic column sum of a row-major [rows][cols] matrix (row pitch ld):

@@ -30,10 +30,22 @@ static unsigned grid_1d(int64_t total, int per_block = 256) {
 constexpr int SM_REG = 16;  // values per lane for the wave-per-row path
 
 // y16 / dx16 (optional): the RNE bf16 copy of the result, for the bf16 GEMM that reads it
-// (attention probabilities into P.V, the score gradient into dQ / dK; bf16 storage)
+// (attention probabilities into P.V, the score gradient into dQ / dK; bf16 storage).
+// SmDrop (seed non-null): y16 holds the dropped-out probabilities instead -- element
+// (row, c) kept when uniform01(seed[0] + add, offset + row * cols + c) >= p, kept values
+// times inv -- the bf16 copy mdemi_dropout_dev16 would write from y, so P.V reads it with no
+// dropout sweep and no fp32 copy of the dropped probabilities (y stays the softmax).
+struct SmDrop {
+  const uint64_t* seed;
+  uint64_t add, offset;
+  float p, inv;
+};
+__device__ __forceinline__ float sm_drop16(const SmDrop& d, uint64_t seed, uint64_t idx, float o) {
+  return d.seed ? (uniform01(seed, d.offset + idx) >= d.p ? o * d.inv : 0.f) : o;
+}
 __global__ __launch_bounds__(256) void softmax_wave_fwd(const float* __restrict__ x, float* __restrict__ y,
                                                         int64_t rows, int cols, float scale,
-                                                        __bf16* __restrict__ y16) {
+                                                        __bf16* __restrict__ y16, SmDrop dr) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -56,18 +68,19 @@ __global__ __launch_bounds__(256) void softmax_wave_fwd(const float* __restrict_
   s = wave_sum(s);
   const float inv = 1.f / s;
   float* yr = y + row * cols;
+  const uint64_t dseed = dr.seed ? dr.seed[0] + dr.add : 0;
 #pragma unroll
   for (int i = 0; i < SM_REG; ++i) {
     const int c = lane + 64 * i;
     if (c < cols) {
       yr[c] = v[i] * inv;
-      if (y16) y16[row * cols + c] = (__bf16)(v[i] * inv);
+      if (y16) y16[row * cols + c] = (__bf16)sm_drop16(dr, dseed, (uint64_t)(row * cols + c), v[i] * inv);
     }
   }
 }
 
 __global__ __launch_bounds__(256) void softmax_block_fwd(const float* __restrict__ x, float* __restrict__ y, int cols,
-                                                         float scale, __bf16* __restrict__ y16) {
+                                                         float scale, __bf16* __restrict__ y16, SmDrop dr) {
   __shared__ float red[8];
   const int64_t row = blockIdx.x;
   const float* xr = x + row * cols;
@@ -96,10 +109,11 @@ __global__ __launch_bounds__(256) void softmax_block_fwd(const float* __restrict
   for (int i = 0; i < 4; ++i) gs += red[4 + i] * __expf(red[i] - gm);
   const float inv = 1.f / gs;
   float* yr = y + row * cols;
+  const uint64_t dseed = dr.seed ? dr.seed[0] + dr.add : 0;
   for (int c = threadIdx.x; c < cols; c += 256) {
     const float o = __expf(scale * xr[c] - gm) * inv;
     yr[c] = o;
-    if (y16) y16[row * cols + c] = (__bf16)o;
+    if (y16) y16[row * cols + c] = (__bf16)sm_drop16(dr, dseed, (uint64_t)(row * cols + c), o);
   }
 }
 
@@ -154,15 +168,8 @@ __global__ __launch_bounds__(256) void softmax_block_bwd(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// dropout: keep(i) = u(seed, offset + i) >= p, u from a splitmix64 finalizer
+// dropout: keep(i) = uniform01(seed, offset + i) >= p (common.h)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t ctr) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(uint32_t)(z >> 40) * (1.f / 16777216.f);
-}
 
 __global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
                                                       float p, float inv_keep, uint64_t seed, uint64_t offset) {
@@ -611,16 +618,30 @@ extern "C" int mdemi_softmax_fwd(const float* x, float* y, int64_t rows, int32_t
   return mdemi_softmax_fwd16(x, y, nullptr, rows, cols, scale, stream);
 }
 
+static int softmax_fwd_launch(const float* x, float* y, void* y16, int64_t rows, int32_t cols, float scale,
+                              const SmDrop& dr, hipStream_t st) {
+  if (cols <= 64 * SM_REG)
+    hipLaunchKernelGGL(softmax_wave_fwd, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, st, x, y, rows, cols, scale,
+                       (__bf16*)y16, dr);
+  else
+    hipLaunchKernelGGL(softmax_block_fwd, dim3((unsigned)rows), dim3(256), 0, st, x, y, cols, scale, (__bf16*)y16,
+                       dr);
+  return check_launch("softmax_fwd");
+}
+
 extern "C" int mdemi_softmax_fwd16(const float* x, float* y, void* y16, int64_t rows, int32_t cols, float scale,
                                    void* stream) {
   MDEMI_REQUIRE(x && y && rows > 0 && cols > 0, "softmax_fwd: bad args");
-  hipStream_t st = (hipStream_t)stream;
-  if (cols <= 64 * SM_REG)
-    hipLaunchKernelGGL(softmax_wave_fwd, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, st, x, y, rows, cols, scale,
-                       (__bf16*)y16);
-  else
-    hipLaunchKernelGGL(softmax_block_fwd, dim3((unsigned)rows), dim3(256), 0, st, x, y, cols, scale, (__bf16*)y16);
-  return check_launch("softmax_fwd");
+  return softmax_fwd_launch(x, y, y16, rows, cols, scale, SmDrop{nullptr, 0, 0, 0.f, 1.f}, (hipStream_t)stream);
+}
+
+extern "C" int mdemi_softmax_fwd_drop16(const float* x, float* y, void* y16, int64_t rows, int32_t cols, float scale,
+                                        float p, const uint64_t* seed_dev, uint64_t seed_add, uint64_t offset,
+                                        void* stream) {
+  MDEMI_REQUIRE(x && y && y16 && rows > 0 && cols > 0 && p > 0.f && p < 1.f && seed_dev,
+                "softmax_fwd_drop16: bad args");
+  return softmax_fwd_launch(x, y, y16, rows, cols, scale, SmDrop{seed_dev, seed_add, offset, p, 1.f / (1.f - p)},
+                            (hipStream_t)stream);
 }
 
 extern "C" int mdemi_softmax_bwd(const float* y, const float* dy, float* dx, int64_t rows, int32_t cols, float scale,

@@ -65,6 +65,8 @@ class GemmDesc(ctypes.Structure):
         ("batch_inner", i32), ("_pad1", i32),
         ("a_bstride_inner", i64), ("b_bstride_inner", i64), ("c_bstride_inner", i64),
         ("row_scale", vp), ("row_scale_group", i64),
+        ("drop_seed", vp), ("drop_add", ctypes.c_uint64), ("drop_offset", ctypes.c_uint64),
+        ("drop_p", f32), ("_pad2", i32),
     ]
 
 
@@ -200,6 +202,8 @@ _SIGS = {
     "mdemi_dropout": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "mdemi_dropout_dev": (ctypes.c_int, [vp, vp, i64, f32, vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "mdemi_dropout_dev16": (ctypes.c_int, [vp, vp, vp, i64, f32, vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
+    "mdemi_softmax_fwd_drop16": (ctypes.c_int, [vp, vp, vp, i64, i32, f32, f32, vp, ctypes.c_uint64, ctypes.c_uint64,
+                                                vp]),
     "mdemi_binhead_nhwc_fwd": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, vp]),
     "mdemi_binhead_nhwc_bwd_workspace_size": (sz, [i32, i64, i32]),
     "mdemi_binhead_nhwc_bwd": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, vp, vp]),

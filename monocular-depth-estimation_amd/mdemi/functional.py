@@ -108,6 +108,11 @@ def _draw_seed(device):
     return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
 
 
+# Dropout fused into its producer (GEMM epilogues, the attention softmax sweep): the same masks
+# and values as the standalone sweeps, bit for bit; MDEMI_FUSE_DROPOUT=0 keeps the sweeps (A/B).
+_FUSE_DROP = [os.environ.get("MDEMI_FUSE_DROPOUT", "1") != "0"]
+
+
 def _drop(src_ptr, dst_ptr, n, p, seed, add=0, offset=0, dst16_ptr=None):
     """Inverted dropout of n floats; mask = hash(seed[0] + add, offset + i); dst16_ptr: also
     the bf16 copy of the result."""
@@ -268,13 +273,18 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
          res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0, rowsum_a=None,
-         a_off=0, b_off=0, c_off=0, inner=None, row_scale=None, row_scale_group=0, a16=None, b16=None, c16=None):
+         a_off=0, b_off=0, c_off=0, inner=None, row_scale=None, row_scale_group=0, a16=None, b16=None, c16=None,
+         drop=None):
     """a_off/b_off/c_off: element offsets into A/B/C (column slices of wider buffers).
     inner=(n, a_bstride_inner, b_bstride_inner, c_bstride_inner): a two-level batch of
     batch = outer * n entries (mdemi_gemm_desc.batch_inner), e.g. (image, head).
     a16 / b16 / c16 (precision "bf16" only): bf16 copies of A / B (the RNE bf16 of the fp32
     tensors, same layout; A / B may then be None) and a bf16 copy of C to write -- the bf16
-    storage path (mdemi_gemm_bf16x), bit-identical to the fp32-operand bf16 GEMM."""
+    storage path (mdemi_gemm_bf16x), bit-identical to the fp32-operand bf16 GEMM.  With A (or
+    B) None only the bf16 copy exists: B16Unsupported is raised (before any launch) when the
+    bf16 loaders cannot stage this layout.
+    drop=(p, seed, add, offset): inverted dropout fused in the epilogue (mdemi_gemm_desc.drop_seed),
+    the mask _drop(C, p, seed, add, offset) would apply over a contiguous C."""
     if inner is not None and inner[0] > 1 and os.environ.get("MDEMI_GEMM_SPLIT_INNER") == "1":
         # debug/A-B path: the same products as one launch per inner index
         n, a2, b2, c2 = inner
@@ -306,6 +316,9 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
         d.rowsum_a = rowsum_a.data_ptr()
     if row_scale is not None:
         d.row_scale, d.row_scale_group = row_scale.data_ptr(), row_scale_group
+    if drop is not None:
+        d.drop_p, d.drop_add, d.drop_offset = float(drop[0]), int(drop[2]), int(drop[3])
+        d.drop_seed = drop[1].data_ptr()
     lib = L.load()
     need = lib.mdemi_gemm_workspace_size(ctypes.byref(d))
     if need:
@@ -330,6 +343,10 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
             if need:
                 ws = L.workspace(need, C.device, slot=1)
                 d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
+    if (A is None or B is None) and not lib.mdemi_gemm_bf16x_supported(
+            ctypes.byref(d), None if a16 is None else a16.data_ptr() + 2 * a_off,
+            None if b16 is None else b16.data_ptr() + 2 * b_off):
+        raise B16Unsupported("gemm: no bf16 path for this layout and no fp32 operand to fall back on")
     LAST_GEMM[0] = "b16" if (a16 is not None and b16 is not None) else _PRECISION[0]
     if a16 is not None or b16 is not None or c16 is not None:
         if _PRECISION[0] != "bf16":
@@ -344,6 +361,11 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     else:
         L.check(lib.mdemi_gemm_f32(ctypes.byref(d), L.stream()), "gemm_f32")
     return C
+
+
+class B16Unsupported(RuntimeError):
+    """gemm() given only the bf16 copy of an operand whose layout the bf16 loaders cannot stage
+    (what mdemi_gemm_bf16x itself refuses with "no bf16 path"), raised before any launch."""
 
 
 def _b16_operands(d, A, B, a_off, b_off, rowsum_a, lib):
@@ -382,9 +404,11 @@ def colsum(x2d, out=None, accumulate=False):
 # --------------------------------------------------------------------------
 
 
-def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NONE, out=None, drop_scale=None):
+def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NONE, out=None, drop_scale=None,
+                   drop=None):
     """drop_scale: per-sample DropPath scale [B] of the product (rows grouped M / B per sample),
-    applied in the epilogue before the residual add."""
+    applied in the epilogue before the residual add; drop: gemm()'s fused dropout (before the
+    residual add)."""
     M, K = x2.shape
     N = weight.shape[0]
     if out is None:
@@ -393,7 +417,8 @@ def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NON
          b_layout=L.L_KCONTIG, a_op=L.OP_GELU if in_gelu else L.OP_NONE,
          bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act,
          residual=residual, ldres=(residual.stride(0) if residual is not None else 0), split_k=1,
-         row_scale=drop_scale, row_scale_group=(M // drop_scale.numel() if drop_scale is not None else 0))
+         row_scale=drop_scale, row_scale_group=(M // drop_scale.numel() if drop_scale is not None else 0),
+         drop=drop)
     return out
 
 
@@ -407,12 +432,16 @@ def _drop_rows(dy2, scale):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, in_gelu, drop_scale):
+    def forward(ctx, x, weight, bias, residual, in_gelu, drop_scale, drop):
+        """drop = (p, seed, offset): y = dropout(x W^T + b) (+ residual) with the dropout in the
+        epilogue -- the mask mf.dropout would draw over the product (its seed and offset)."""
         _require_cuda(x, weight, bias, residual)
         K = x.shape[-1]
         x2 = _c(x).reshape(-1, K)
         res2 = _c(residual).reshape(x2.shape[0], -1) if residual is not None else None
-        out = linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2, drop_scale=drop_scale)
+        out = linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2, drop_scale=drop_scale,
+                             drop=None if drop is None else (drop[0], drop[1], 0, drop[2]))
+        ctx.drop = drop
         ctx.save_for_backward(x2, weight)
         ctx.dx16 = grad_feeds_gemm(x)
         ctx.drop_scale = drop_scale
@@ -430,6 +459,14 @@ class _LinearFn(torch.autograd.Function):
         dy2 = _c(dy).reshape(M, N)
         if ctx.drop_scale is not None:  # the branch's gradient; the residual's stays dy
             dy2 = _drop_rows(dy2, ctx.drop_scale)
+        if ctx.drop is not None:  # the dropout backward: the product's gradient (+ its bf16 copy)
+            p, seed, off = ctx.drop
+            d = torch.empty_like(dy2)
+            d16 = new_b16_like(d) if (d.numel() % 4 == 0 and dy2.data_ptr() % 16 == 0) else None
+            _drop(dy2.data_ptr(), d.data_ptr(), d.numel(), p, seed, offset=off, dst16_ptr=L.ptr(d16))
+            if d16 is not None:
+                set_b16(d, d16)
+            dy2 = d
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, device=dy.device, dtype=torch.float32)
@@ -452,15 +489,29 @@ class _LinearFn(torch.autograd.Function):
         elif want_db:
             colsum(dy2, out=db)
         dres = dy if ctx.has_res and ctx.needs_input_grad[3] else None
-        return dx, dw, db, dres, None, None
+        return dx, dw, db, dres, None, None, None
 
 
-def linear(x, weight, bias=None, residual=None, in_gelu=False, drop_scale=None):
+def linear(x, weight, bias=None, residual=None, in_gelu=False, drop_scale=None, p=0.0, training=False):
     """y = (gelu(x) if in_gelu else x) @ W^T + b (+ residual); drop_scale (DropPath, per
-    sample [B]): y = residual + drop_scale[sample] * (x @ W^T + b), fused in the epilogue."""
+    sample [B]): y = residual + drop_scale[sample] * (x @ W^T + b), fused in the epilogue.
+    p > 0 and training: y = dropout(x @ W^T + b) (+ residual) -- nn.Dropout on a projection's
+    output before a residual add (luna_layer.py:172-173,250-251, self_attention.py:78-80) --
+    with the dropout in the epilogue (same seed draw, offset and mask as mf.dropout)."""
     if drop_scale is not None and residual is None:
         raise ValueError("linear: drop_scale scales a residual branch and needs residual")
-    return _LinearFn.apply(x, weight, bias, residual, in_gelu, drop_scale)
+    if training and p > 0.0:
+        if drop_scale is not None:
+            raise ValueError("linear: dropout and drop_scale together are not supported")
+        if not _FUSE_DROP[0]:
+            y = dropout(_LinearFn.apply(x, weight, bias, None, in_gelu, None, None), p, True)
+            return add(residual, y) if residual is not None else y
+        n = x.numel() // x.shape[-1] * weight.shape[0]
+        seed = _draw_seed(x.device)
+        off = _drop_counter[0]
+        _drop_counter[0] += n
+        return _LinearFn.apply(x, weight, bias, residual, in_gelu, None, (float(p), seed, off))
+    return _LinearFn.apply(x, weight, bias, residual, in_gelu, drop_scale, None)
 
 
 class _MlpFn(torch.autograd.Function):
@@ -485,15 +536,20 @@ class _MlpFn(torch.autograd.Function):
         h = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
         g = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
         g16 = new_b16_like(g) if g.numel() % 4 == 0 else None  # fc2's operand (bf16 storage)
+        fuse = _FUSE_DROP[0]
+        # fused: g = dropout(act(fc1(x))) and its bf16 copy from fc1's epilogue (same mask)
         gemm(x2, _c(w1), g, M, Hd, K, lda=K, ldb=K, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
              bias=b1, bias_mode=L.BIAS_COL if b1 is not None else L.BIAS_NONE, act=act,
-             preact=h, ldpre=Hd, split_k=1, c16=g16 if p_mid == 0.0 else None)
-        if p_mid > 0.0:
+             preact=h, ldpre=Hd, split_k=1, c16=g16 if (p_mid == 0.0 or fuse) else None,
+             drop=(p_mid, seed, 0, 0) if (p_mid > 0.0 and fuse) else None)
+        if p_mid > 0.0 and not fuse:
             _drop(g.data_ptr(), g.data_ptr(), g.numel(), p_mid, seed, dst16_ptr=L.ptr(g16))
         if g16 is not None:
             set_b16(g, g16)
         res2 = _c(residual).reshape(M, N) if residual is not None else None
-        if p_out > 0.0:
+        if p_out > 0.0 and fuse:  # out = dropout(fc2(g)) + residual in fc2's epilogue
+            out = linear_fwd_raw(g, _c(w2), b2, residual=res2, drop=(p_out, seed, 1, 0))
+        elif p_out > 0.0:
             out = linear_fwd_raw(g, _c(w2), b2)
             _drop(out.data_ptr(), out.data_ptr(), out.numel(), p_out, seed, add=1)
             if res2 is not None:
@@ -531,15 +587,16 @@ class _MlpFn(torch.autograd.Function):
         gemm(d2, g, dw2, N, Hd, M, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
              rowsum_a=db2)
         dh = torch.empty(M, Hd, device=dev, dtype=torch.float32)
-        if p_mid > 0.0:
+        if p_mid > 0.0 and not _FUSE_DROP[0]:
             gemm(d2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
             _drop(dh.data_ptr(), dh.data_ptr(), dh.numel(), p_mid, seed)
             L.call("mdemi_elementwise", L.EW_ACT_BWD, h.data_ptr(), dh.data_ptr(), dh.data_ptr(), dh.numel(),
                    float(act), 0.0, L.stream())
-        else:
+        else:  # fused: dh = act'(h) * dropout_bwd(d2 . W2) in the dgrad epilogue (mask of the forward's)
             dh16 = new_b16_like(dh)  # the operand of both fc1 gradient GEMMs
             gemm(d2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
-                 act=L.ACT_GRAD_OF[act], aux=h, ldaux=Hd, c16=dh16)
+                 act=L.ACT_GRAD_OF[act], aux=h, ldaux=Hd, c16=dh16,
+                 drop=(p_mid, seed, 0, 0) if p_mid > 0.0 else None)
             if dh16 is not None:
                 set_b16(dh, dh16)
         del h, g
@@ -618,69 +675,113 @@ class _Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, y = ctx.saved_tensors
-        stride, pad, pad_mode, act, has_bias, pointwise = ctx.cfg
-        dy = _c(dy)
-        if act != L.ACT_NONE:
-            if act != L.ACT_RELU:
-                raise NotImplementedError("conv2d backward: only ReLU epilogue supported")
-            g = torch.empty_like(dy)
-            L.call("mdemi_elementwise", L.EW_ACT_BWD, y.data_ptr(), dy.data_ptr(), g.data_ptr(), dy.numel(),
-                   float(L.ACT_RELU), 0.0, L.stream())
-            dy = g
-        n, h, w, c = x.shape
-        cout, cin, kh, kw = weight.shape
-        _, oh, ow, _ = dy.shape
-        M, K = n * oh * ow, kh * kw * c
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            if pointwise:
-                dx = torch.empty_like(x)
-                gemm(dy, weight.reshape(cout, cin), dx, M, c, cout, lda=cout, ldb=cin, ldc=c,
-                     a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
-            elif stride == kh == kw and pad == 0 and not ctx.explicit:
-                # non-overlapping patches (mViT embedding_encoder): column gradients by one GEMM
-                # against the (ky,kx,c)-ordered weight, then a scatter back to the NHWC pixels
-                wf = conv_weight_layout(weight, L.WL_OHWI).view(cout, K)
-                dcols = torch.empty(M, K, device=dy.device, dtype=torch.float32)
-                gemm(dy, wf, dcols, M, K, cout, lda=cout, ldb=K, ldc=K, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
-                dx = torch.empty_like(x)
-                L.call("mdemi_unpatchify_nhwc", dcols.data_ptr(), dx.data_ptr(), n, h, w, c, stride, oh, ow,
-                       L.stream())
+        return _conv2d_backward(ctx, dy, None)
+
+
+def _conv2d_backward(ctx, dy, dskip):
+    """_Conv2dFn's backward; dskip (pointwise only): the gradient of the conv's input through a
+    residual skip, added in the input-gradient GEMM's epilogue."""
+    x, weight, y = ctx.saved_tensors
+    stride, pad, pad_mode, act, has_bias, pointwise = ctx.cfg
+    dy = _c(dy)
+    if act != L.ACT_NONE:
+        if act != L.ACT_RELU:
+            raise NotImplementedError("conv2d backward: only ReLU epilogue supported")
+        g = torch.empty_like(dy)
+        L.call("mdemi_elementwise", L.EW_ACT_BWD, y.data_ptr(), dy.data_ptr(), g.data_ptr(), dy.numel(),
+               float(L.ACT_RELU), 0.0, L.stream())
+        dy = g
+    n, h, w, c = x.shape
+    cout, cin, kh, kw = weight.shape
+    _, oh, ow, _ = dy.shape
+    M, K = n * oh * ow, kh * kw * c
+    dx = dw = db = None
+    if ctx.needs_input_grad[0]:
+        if pointwise:
+            dx = torch.empty_like(x)
+            gemm(dy, weight.reshape(cout, cin), dx, M, c, cout, lda=cout, ldb=cin, ldc=c,
+                 a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG, residual=dskip, ldres=c if dskip is not None else 0)
+        elif dskip is not None:
+            raise NotImplementedError("conv2d skip: pointwise convs only")
+        elif stride == kh == kw and pad == 0 and not ctx.explicit:
+            # non-overlapping patches (mViT embedding_encoder): column gradients by one GEMM
+            # against the (ky,kx,c)-ordered weight, then a scatter back to the NHWC pixels
+            wf = conv_weight_layout(weight, L.WL_OHWI).view(cout, K)
+            dcols = torch.empty(M, K, device=dy.device, dtype=torch.float32)
+            gemm(dy, wf, dcols, M, K, cout, lda=cout, ldb=K, ldc=K, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
+            dx = torch.empty_like(x)
+            L.call("mdemi_unpatchify_nhwc", dcols.data_ptr(), dx.data_ptr(), n, h, w, c, stride, oh, ow,
+                   L.stream())
+        else:
+            if stride != 1 or ctx.explicit:
+                raise NotImplementedError("conv2d dgrad: stride 1 or stride == kernel only")
+            # dX = conv(dY, flip(W)^T) with pad k-1-p:  Wd[(ky,kx,co)][c] = W[co][c][k-1-ky][k-1-kx]
+            wd = conv_weight_layout(weight, L.WL_DGRAD).view(kh * kw * cout, cin)
+            dx = torch.empty_like(x)
+            if pad_mode == L.PAD_ZERO:
+                gemm(dy, wd, dx, n * h * w, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
+                     b_layout=L.L_MNCONTIG,
+                     conv=_geom(n, oh, ow, cout, h, w, kh, kw, 1, kh - 1 - pad, L.PAD_ZERO))
             else:
-                if stride != 1 or ctx.explicit:
-                    raise NotImplementedError("conv2d dgrad: stride 1 or stride == kernel only")
-                # dX = conv(dY, flip(W)^T) with pad k-1-p:  Wd[(ky,kx,co)][c] = W[co][c][k-1-ky][k-1-kx]
-                wd = conv_weight_layout(weight, L.WL_DGRAD).view(kh * kw * cout, cin)
-                dx = torch.empty_like(x)
-                if pad_mode == L.PAD_ZERO:
-                    gemm(dy, wd, dx, n * h * w, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
-                         b_layout=L.L_MNCONTIG,
-                         conv=_geom(n, oh, ow, cout, h, w, kh, kw, 1, kh - 1 - pad, L.PAD_ZERO))
-                else:
-                    # replicate padding (layer_utils.py:21): gradient of the padded input by a full
-                    # correlation, then fold the border rows/columns onto the edge pixels
-                    hp, wp = h + 2 * pad, w + 2 * pad
-                    dxp = torch.empty(n, hp, wp, c, device=dy.device, dtype=torch.float32)
-                    gemm(dy, wd, dxp, n * hp * wp, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
-                         b_layout=L.L_MNCONTIG,
-                         conv=_geom(n, oh, ow, cout, hp, wp, kh, kw, 1, kh - 1, L.PAD_ZERO))
-                    L.call("mdemi_pad_fold_replicate", dxp.data_ptr(), dx.data_ptr(), n, h, w, c, pad, L.stream())
-        want_db = has_bias and ctx.needs_input_grad[2]
-        if want_db:
-            db = torch.empty(cout, device=dy.device, dtype=torch.float32)
-        if ctx.needs_input_grad[1]:
-            dwf = torch.empty(cout, K, device=dy.device, dtype=torch.float32)
-            if pointwise:
-                gemm(dy, x, dwf, cout, K, M, lda=cout, ldb=c, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
-                     rowsum_a=db)
-            else:
-                gemm(dy, x, dwf, cout, K, M, lda=cout, ldb=0, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_CONV,
-                     conv=_geom(n, h, w, c, oh, ow, kh, kw, stride, pad, pad_mode), rowsum_a=db)
-            dw = conv_weight_layout(dwf, L.WL_OIHW, (cout, cin, kh, kw))
-        elif want_db:
-            colsum(dy.reshape(-1, cout), out=db)
-        return dx, dw, db, None, None, None, None, None
+                # replicate padding (layer_utils.py:21): gradient of the padded input by a full
+                # correlation, then fold the border rows/columns onto the edge pixels
+                hp, wp = h + 2 * pad, w + 2 * pad
+                dxp = torch.empty(n, hp, wp, c, device=dy.device, dtype=torch.float32)
+                gemm(dy, wd, dxp, n * hp * wp, c, kh * kw * cout, lda=0, ldb=cin, ldc=c, a_layout=L.L_CONV,
+                     b_layout=L.L_MNCONTIG,
+                     conv=_geom(n, oh, ow, cout, hp, wp, kh, kw, 1, kh - 1, L.PAD_ZERO))
+                L.call("mdemi_pad_fold_replicate", dxp.data_ptr(), dx.data_ptr(), n, h, w, c, pad, L.stream())
+    want_db = has_bias and ctx.needs_input_grad[2]
+    if want_db:
+        db = torch.empty(cout, device=dy.device, dtype=torch.float32)
+    if ctx.needs_input_grad[1]:
+        dwf = torch.empty(cout, K, device=dy.device, dtype=torch.float32)
+        if pointwise:
+            gemm(dy, x, dwf, cout, K, M, lda=cout, ldb=c, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+                 rowsum_a=db)
+        else:
+            gemm(dy, x, dwf, cout, K, M, lda=cout, ldb=0, ldc=K, a_layout=L.L_MNCONTIG, b_layout=L.L_CONV,
+                 conv=_geom(n, h, w, c, oh, ow, kh, kw, stride, pad, pad_mode), rowsum_a=db)
+        dw = conv_weight_layout(dwf, L.WL_OIHW, (cout, cin, kh, kw))
+    elif want_db:
+        colsum(dy.reshape(-1, cout), out=db)
+    return dx, dw, db, None, None, None, None, None
+
+
+class _Conv2dSkipFn(torch.autograd.Function):
+    """x -> (conv1x1(x), x): a pointwise conv whose input is also its block's residual
+    (EfficientNet InvertedResidual: conv_pw(x) ... + x, gen-efficientnet via
+    unet_adaptive_bins.py:129 / depthformer_v8.py:89).  The two gradient contributions to x meet
+    in the input-gradient GEMM's epilogue (residual = the skip's gradient) instead of an autograd
+    add over the block input; the sum is the same fp32 addition, so results are unchanged."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        out = _Conv2dFn.forward(ctx, x, weight, None, 1, 0, L.PAD_ZERO, L.ACT_NONE)
+        ctx.set_materialize_grads(False)
+        return out, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dskip):
+        if dy is None:
+            return dskip, None
+        dskip = _c(dskip) if dskip is not None else None
+        dx, dw, _ = _conv2d_backward(ctx, dy, dskip)[:3]
+        return dx, dw
+
+
+# MDEMI_CONV_SKIP=0: the autograd add instead (A/B and the bit-identity test)
+_FUSE_SKIP = [os.environ.get("MDEMI_CONV_SKIP", "1") != "0"]
+
+
+def conv2d_nhwc_skip(x, weight):
+    """(conv1x1(x), x) for a residual block whose first op is a bias-free pointwise conv: use the
+    second output as the block's skip, so the input gradient is one GEMM epilogue."""
+    if weight.shape[-1] != 1 or weight.shape[-2] != 1:
+        raise ValueError("conv2d_nhwc_skip: pointwise (1x1) convs only")
+    if not _FUSE_SKIP[0]:
+        return _Conv2dFn.apply(x, weight, None, 1, 0, L.PAD_ZERO, L.ACT_NONE), x
+    return _Conv2dSkipFn.apply(x, weight)
 
 
 class _HeadConvFn(torch.autograd.Function):
@@ -1949,19 +2050,36 @@ class _AttentionFn(torch.autograd.Function):
         # bf16 storage: the probabilities' bf16 copy (P.V's operand) from the softmax sweep, or the
         # dropped-out ones' from the dropout sweep
         P16 = new_b16_like(P) if (p == 0.0 or P.numel() % 4 == 0) else None
-        L.call("mdemi_softmax_fwd16", P.data_ptr(), P.data_ptr(), L.ptr(P16) if p == 0.0 else None,
-               B * heads * Sq, Sk, float(scale), L.stream())
-        Pd = P
-        if p > 0.0:
-            Pd = torch.empty_like(P)
-            _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed, dst16_ptr=L.ptr(P16))
-        if P16 is not None:
-            set_b16(Pd, P16)
         out = torch.empty(B * Sq, heads * dv, device=dev, dtype=torch.float32)
         out16 = new_b16_like(out) if out_b16 else None  # the output projection's operand
-        gemm(Pd, vsrc, out, Sq, dv, Sk, lda=Sk, ldb=ldv, ldc=heads * dv, a_layout=L.L_KCONTIG,
-             b_layout=L.L_MNCONTIG, batch=B * heads, a_bstride=heads * hs, b_bstride=Sk * ldv,
-             c_bstride=Sq * heads * dv, b_off=v_off, inner=(heads, hs, dv, dv), c16=out16)
+        pv = dict(lda=Sk, ldb=ldv, ldc=heads * dv, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG, batch=B * heads,
+                  a_bstride=heads * hs, b_bstride=Sk * ldv, c_bstride=Sq * heads * dv, b_off=v_off,
+                  inner=(heads, hs, dv, dv), c16=out16)
+        ctx.P16d = None
+        v16 = b16_of(vsrc) if (p > 0.0 and P16 is not None and _FUSE_DROP[0]) else None
+        softmaxed = False  # P holds softmax(scale * P) already (the sweep runs in place: never twice)
+        if v16 is not None:
+            # fused attention dropout (bf16 storage): the softmax sweep writes P and the bf16 copy of
+            # dropout(P), P.V reads that copy; no dropout sweep, no fp32 dropout(P)
+            L.call("mdemi_softmax_fwd_drop16", P.data_ptr(), P.data_ptr(), P16.data_ptr(), B * heads * Sq, Sk,
+                   float(scale), float(p), seed.data_ptr(), 0, 0, L.stream())
+            softmaxed = True
+            try:
+                gemm(None, vsrc, out, Sq, dv, Sk, a16=P16, b16=v16, **pv)
+                ctx.P16d = P16  # dropout(P) in bf16: dV's operand in the backward
+            except B16Unsupported:  # V's bf16 slice cannot be staged: the fp32 dropout(P) below
+                v16 = None
+        if v16 is None:
+            if not softmaxed:
+                L.call("mdemi_softmax_fwd16", P.data_ptr(), P.data_ptr(), L.ptr(P16) if p == 0.0 else None,
+                       B * heads * Sq, Sk, float(scale), L.stream())
+            Pd = P
+            if p > 0.0:
+                Pd = torch.empty_like(P)
+                _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed, dst16_ptr=L.ptr(P16))
+            if P16 is not None:
+                set_b16(Pd, P16)
+            gemm(Pd, vsrc, out, Sq, dv, Sk, **pv)
         if out16 is not None:
             set_b16(out, out16)
         ctx.save_for_backward(qsrc, ksrc, vsrc, P)
@@ -1976,10 +2094,13 @@ class _AttentionFn(torch.autograd.Function):
         B, Sq, Sk, heads, dqk, dv, q_off, k_off, v_off, scale, p, seed = ctx.cfg
         ldq, ldk, ldv = qsrc.shape[-1], ksrc.shape[-1], vsrc.shape[-1]
         hs = Sq * Sk
-        Pd = P
-        if p > 0.0:
+        Pd, Pd16 = P, None
+        if p > 0.0 and ctx.P16d is not None:
+            Pd, Pd16 = None, ctx.P16d  # the forward's bf16 dropout(P): dV's operand, no regeneration
+        elif p > 0.0:
             Pd = torch.empty_like(P)
             _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed)
+        ctx.P16d = None
         # one gradient buffer per distinct source tensor; columns outside the used slices are zero
         bufs, spans, b16s = {}, {}, {}
         for t, off, width in ((qsrc, q_off, heads * dqk), (ksrc, k_off, heads * dqk), (vsrc, v_off, heads * dv)):
@@ -2000,13 +2121,23 @@ class _AttentionFn(torch.autograd.Function):
         dP = torch.empty_like(P)
         if dout is not None:
             dout = _c(dout)
+            fuse = p > 0.0 and _FUSE_DROP[0]  # dP = dropout_bwd(dO . V^T) in the GEMM epilogue
             gemm(dout, vsrc, dP, Sq, Sk, dv, lda=heads * dv, ldb=ldv, ldc=Sk, a_layout=L.L_KCONTIG,
                  b_layout=L.L_KCONTIG, batch=B * heads, a_bstride=Sq * heads * dv, b_bstride=Sk * ldv,
-                 c_bstride=heads * hs, b_off=v_off, inner=(heads, dv, dv, hs))
-            gemm(Pd, dout, dvv, Sk, dv, Sq, lda=Sk, ldb=heads * dv, ldc=ldv, a_layout=L.L_MNCONTIG,
-                 b_layout=L.L_MNCONTIG, batch=B * heads, a_bstride=heads * hs, b_bstride=Sq * heads * dv,
-                 c_bstride=Sk * ldv, c_off=v_off, inner=(heads, hs, dv, dv), c16=dv16)
-            if p > 0.0:
+                 c_bstride=heads * hs, b_off=v_off, inner=(heads, dv, dv, hs), drop=(p, seed, 0, 0) if fuse else None)
+            dvk = dict(lda=Sk, ldb=heads * dv, ldc=ldv, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
+                       batch=B * heads, a_bstride=heads * hs, b_bstride=Sq * heads * dv, c_bstride=Sk * ldv,
+                       c_off=v_off, inner=(heads, hs, dv, dv), c16=dv16)
+            o16 = b16_of(dout) if Pd16 is not None else None
+            try:
+                if o16 is None and Pd16 is not None:
+                    raise B16Unsupported("dO has no bf16 copy")
+                gemm(Pd, dout, dvv, Sk, dv, Sq, a16=Pd16, b16=o16, **dvk)
+            except B16Unsupported:  # regenerate dropout(P) in fp32 instead
+                Pd = torch.empty_like(P)
+                _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed)
+                gemm(Pd, dout, dvv, Sk, dv, Sq, **dvk)
+            if p > 0.0 and not fuse:
                 _drop(dP.data_ptr(), dP.data_ptr(), dP.numel(), p, seed)
             if dP_ext is not None:
                 dP_ext = _c(dP_ext)

@@ -21,11 +21,8 @@ def transformer_encoder_layer(layer: nn.TransformerEncoderLayer, t, B, S, traini
     qkv = mf.linear(t, sa.in_proj_weight, sa.in_proj_bias)
     o, _ = mf.attention(qkv, qkv, qkv, B, S, S, heads, hd, hd, hd ** -0.5, q_off=0, k_off=E, v_off=2 * E,
                         p=sa.dropout, training=training)
-    p1 = layer.dropout1.p if training else 0.0
-    if p1 > 0.0:
-        x = mf.add(t, mf.dropout(mf.linear(o, sa.out_proj.weight, sa.out_proj.bias), p1, True))
-    else:
-        x = mf.linear(o, sa.out_proj.weight, sa.out_proj.bias, residual=t)
+    # t + dropout1(out_proj(o)): dropout and residual add in the projection's epilogue
+    x = mf.linear(o, sa.out_proj.weight, sa.out_proj.bias, residual=t, p=layer.dropout1.p, training=training)
     x = mf.layer_norm(x, layer.norm1.weight, layer.norm1.bias, layer.norm1.eps)
     y = mf.mlp(x, layer.linear1.weight, layer.linear1.bias, layer.linear2.weight, layer.linear2.bias, residual=x,
                act=L.ACT_RELU, p_mid=layer.dropout.p, p_out=layer.dropout2.p, training=training)

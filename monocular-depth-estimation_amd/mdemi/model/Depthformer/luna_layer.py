@@ -56,8 +56,7 @@ class PreNormLunaBlock(nn.Module):
         kvq = mf.linear(hidden_n, w_h, b_h)                                                  # (B*HW, qk+d+qk)
         out1, attn1 = mf.attention(q1, kvq, kvq, B, K, HW, nh, qk // nh, d // nh, self.attn_scale, q_off=0,
                                    k_off=0, v_off=qk, p=self.attn_drop.p, training=tr, out_b16=True)
-        out1 = mf.linear(out1, self.o1_proj.weight, self.o1_proj.bias)                      # (B*K, a)
-        out1 = mf.dropout(out1, self.drop.p, tr)
+        out1 = mf.linear(out1, self.o1_proj.weight, self.o1_proj.bias, p=self.drop.p, training=tr)  # (B*K, a)
         aux_out = mf.add(aux, out1)
         out_n = mf.layer_norm(out1, self.inter_norm.weight, self.inter_norm.bias, self.inter_norm.eps,
                                   out_b16=True)
@@ -66,11 +65,8 @@ class PreNormLunaBlock(nn.Module):
         kv2 = mf.linear(out_n, w_a, b_a)                                                     # (B*K, qk+d)
         out2, attn2 = mf.attention(kvq, kv2, kv2, B, HW, K, nh, qk // nh, d // nh, self.attn_scale,
                                    q_off=qk + d, k_off=0, v_off=qk, p=self.attn_drop.p, training=tr, out_b16=True)
-        if tr and self.drop.p > 0.0:
-            out2 = mf.dropout(mf.linear(out2, self.o2_proj.weight, self.o2_proj.bias), self.drop.p, True)
-            out = mf.add(hidden, out2)
-        else:
-            out = mf.linear(out2, self.o2_proj.weight, self.o2_proj.bias, residual=hidden)
+        # hidden + dropout(o2_proj(out2)): the dropout and the residual add in the projection's epilogue
+        out = mf.linear(out2, self.o2_proj.weight, self.o2_proj.bias, residual=hidden, p=self.drop.p, training=tr)
         return out, aux_out, attn1, attn2
 
 

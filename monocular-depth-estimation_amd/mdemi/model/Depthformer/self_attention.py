@@ -37,11 +37,9 @@ class SelfAttentionBlock(nn.Module):
         qkv = mf.linear(h, w, b)
         o, attn = mf.attention(qkv, qkv, qkv, B, S, S, nh, kq // nh, d // nh, self.attn_scale, q_off=0, k_off=kq,
                                v_off=2 * kq, p=self.attn_drop.p, training=self.training, out_b16=True)
-        if self.training and self.drop.p > 0.0:
-            out = mf.add(mf.dropout(mf.linear(o, self.out_proj.weight, self.out_proj.bias), self.drop.p, True),
-                         hidden)
-        else:
-            out = mf.linear(o, self.out_proj.weight, self.out_proj.bias, residual=hidden)
+        # hidden + dropout(out_proj(o)): dropout and residual add in the projection's epilogue
+        out = mf.linear(o, self.out_proj.weight, self.out_proj.bias, residual=hidden, p=self.drop.p,
+                        training=self.training)
         return out, attn
 
 

@@ -70,6 +70,10 @@ class Conv2dSame(nn.Conv2d):
     def __init__(self, in_chs, out_chs, k, stride=1, groups=1):
         super().__init__(in_chs, out_chs, k, stride=stride, padding=0, groups=groups, bias=False)
 
+    def forward_skip(self, x):
+        """(conv(x), x) of a 1x1 conv whose input is also the block's residual (mf.conv2d_nhwc_skip)."""
+        return mf.conv2d_nhwc_skip(x, self.weight)
+
     def forward(self, x):
         k, s = self.kernel_size[0], self.stride[0]
         if self.groups > 1:
@@ -149,7 +153,11 @@ class InvertedResidual(nn.Module):
         self.bn3._mdemi_out_b16 = not self.has_residual  # the block output feeds the next conv_pw
 
     def forward(self, x):
-        y = self.bn2(self.conv_dw(self.bn1(self.conv_pw(x))))
+        if self.has_residual:  # x's two gradients meet in conv_pw's input-gradient epilogue
+            y, x = self.conv_pw.forward_skip(x)
+        else:
+            y = self.conv_pw(x)
+        y = self.bn2(self.conv_dw(self.bn1(y)))
         y = self.bn3(self.conv_pwl(self.se(y)))
         return _residual(y, x) if self.has_residual else y
 

@@ -33,7 +33,7 @@ Bucket rebuild (``rebuild_buckets``, on by default; torch DDP rebuilds its bucke
 first iteration for the same reason).  Reverse registration order is only a guess at the
 order backward produces gradients: a parameter registered early but used late (NeW-CRFs'
 backbone out-norms, read by the decoder) finishes its bucket late, and strict index order
-then holds every later bucket back (bench.py --ddp measured bucket 4 of the large07 KITTI
+then holds every later bucket back (bench.py --ddp measured bucket 4 of the large07 NYU
 step ready 8 ms before the end of backward, holding back 9 buckets that were ready 18-62 ms
 earlier).  The first synchronised backward records the order the gradients actually land
 in; ``finish()`` then regroups the parameters in that order (rank 0's order, broadcast, so
