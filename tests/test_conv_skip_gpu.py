@@ -50,7 +50,7 @@ def test_efficientnet_step_with_conv_skip_bit_identical(mf, prec):
     m = UnetAdaptiveBins.build(32, 1e-3, 10.0)
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     closed_form_fill(sd, seed=0.29, scale=0.03)
-    img = torch.from_numpy(rng_array((2, 3, 96, 128), 51)).float().to(DEV)
+    img = torch.from_numpy(rng_array((2, 3, 352, 480), 51)).float().to(DEV)  # >= 129 mViT tokens
     m = m.to(DEV).train()
 
     def run(fuse):

@@ -8,5 +8,5 @@ for arm in "$@"; do
   label=${arm%%:*}; rest=${arm#*:}; envs=${rest%%:*}; args=${rest#*:}
   [ "$envs" = "-" ] && envs=""
   env $envs timeout -k 10 300 python -u bench.py $args > gpurun_out/ab_${tag}_$label.log 2>&1 || { echo "arm $label failed"; tail -5 gpurun_out/ab_${tag}_$label.log; exit 1; }
-  echo "$label $(grep '^{"metric' gpurun_out/ab_${tag}_$label.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d.get("roofline",{}).get("achieved"), d.get("gemm_all",{}).get("gemm_ms_per_step"))')"
+  grep "^{\"metric" gpurun_out/ab_${tag}_$label.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(\"$label\", d[\"value\"], d[\"ms_per_step\"])"
 done
