@@ -122,20 +122,6 @@ typedef struct mdemi_gemm_desc {
                                       keep/(1-p) scale of a residual branch
                                       (swin_transformer.py:232,239) fused into the proj /
                                       fc2 epilogue.  Batch 1. */
-  const uint64_t* drop_seed;       /* optional (device pointer): inverted dropout in the
-                                      epilogue, the mask of mdemi_dropout_dev over C: element
-                                      (i, j) of batch entry z, at flat offset
-                                      e = (z's C offset) + i * ldc + j from C, is kept when
-                                      uniform(drop_seed[0] + drop_add, drop_offset + e) >= drop_p
-                                      and scaled by 1 / (1 - drop_p).  Applied to the value
-                                      after a forward `act` (nn.Dropout after the activation:
-                                      feed_forward.py:26, layers.py:8) or, with a *_GRAD act,
-                                      to the product before the act'(aux) multiply (the
-                                      dropout backward between fc2's dgrad and the activation
-                                      gradient); before row_scale and the residual add.
-                                      The bf16 copy c16 is of the dropped-out value. */
-  uint64_t drop_add, drop_offset;
-  float drop_p; int32_t _pad2;
 } mdemi_gemm_desc;
 
 size_t mdemi_gemm_workspace_size(const mdemi_gemm_desc* d);

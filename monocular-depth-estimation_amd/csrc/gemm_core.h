@@ -64,15 +64,7 @@ struct GemmParams {
   int* tile_cnt;  // non-null: the last-arriving split of a tile combines the slabs (no reduce launch)
   float* rowsum_out;  // with tile_cnt and split row-sum partials: the last arriver writes the sums here
   void* c16;  // optional bf16 copy (RNE) of the final output, C's layout: the bf16 operand of a later GEMM
-  // optional epilogue dropout (mdemi_gemm_desc.drop_seed): mask index drop_off + the element's
-  // offset from C, kept values times drop_inv
-  const uint64_t* drop_seed; uint64_t drop_add, drop_off; float drop_p, drop_inv;
 };
-
-// the epilogue dropout of the element at offset e from C (seed = drop_seed[0] + drop_add)
-__device__ __forceinline__ float drop_keep(const GemmParams& p, uint64_t seed, int64_t e, float v) {
-  return uniform01(seed, p.drop_off + (uint64_t)e) >= p.drop_p ? v * p.drop_inv : 0.f;
-}
 
 // One thread's 4 bias-gradient row sums (rows i..i+3) of a K piece: plain stores, or
 // write-through (sc1) stores when the pieces are split (the tile's last arriver may read
@@ -349,14 +341,8 @@ __device__ __forceinline__ float epilogue_value(const GemmParams& p, int b, int 
   if (p.bias_mode == MDEMI_BIAS_COL) v += p.bias[j];
   else if (p.bias_mode == MDEMI_BIAS_ROW) v += p.bias[i];
   if (p.pre) p.pre[(int64_t)b * p.pre_bs + (int64_t)i * p.ldpre + j] = v;
-  const int64_t e = boff(p, b, p.c_bs, p.c_bs2) + (int64_t)i * p.ldc + j;
-  if (is_grad_act(p.act)) {
-    if (p.drop_seed) v = drop_keep(p, p.drop_seed[0] + p.drop_add, e, v);
-    v *= aux_grad(p.act, p.aux[(int64_t)b * p.aux_bs + (int64_t)i * p.ldaux + j]);
-  } else {
-    if (p.act != MDEMI_ACT_NONE) v = apply_act(p.act, v);
-    if (p.drop_seed) v = drop_keep(p, p.drop_seed[0] + p.drop_add, e, v);
-  }
+  if (is_grad_act(p.act)) v *= aux_grad(p.act, p.aux[(int64_t)b * p.aux_bs + (int64_t)i * p.ldaux + j]);
+  else if (p.act != MDEMI_ACT_NONE) v = apply_act(p.act, v);
   if (p.rowscale) v *= p.rowscale[fdiv(i, p.fd_rs)];
   if (p.res) v += p.res[(int64_t)b * p.res_bs + (int64_t)i * p.ldres + j];
   return v;

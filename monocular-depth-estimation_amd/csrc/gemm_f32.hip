@@ -209,7 +209,6 @@ static int validate(const mdemi_gemm_desc* d) {
     MDEMI_REQUIRE(d->N < lim, "gemm: N too large for split-K slabs");
   MDEMI_REQUIRE(!(d->act == MDEMI_ACT_GELU_GRAD || d->act == MDEMI_ACT_RELU_GRAD || d->act == MDEMI_ACT_SILU_GRAD) ||
                     d->aux, "gemm: *_GRAD epilogue needs aux");
-  if (d->drop_seed) MDEMI_REQUIRE(d->drop_p > 0.f && d->drop_p < 1.f, "gemm: drop_p must be in (0, 1)");
   return MDEMI_OK;
 }
 
@@ -286,11 +285,6 @@ static void fill_params(const mdemi_gemm_desc* d, GemmParams& p, int variant, in
   p.tile_cnt = nullptr;
   p.rowsum_out = nullptr;
   p.c16 = nullptr;
-  p.drop_seed = d->drop_seed;
-  p.drop_add = d->drop_add;
-  p.drop_off = d->drop_offset;
-  p.drop_p = d->drop_p;
-  p.drop_inv = d->drop_seed ? 1.f / (1.f - d->drop_p) : 1.f;
   // vector loads need every row start 16-B aligned and whole quads in range
   // (KCONTIG: K % 4; MNCONTIG: the row/column extent % 4)
   p.a_vec = al16(d->A) && (d->lda % 4 == 0) && (d->a_bstride % 4 == 0) && (p.a_bs2 % 4 == 0) &&
@@ -349,7 +343,7 @@ static size_t rowsum_bytes(const mdemi_gemm_desc* d, const GemmParams& p) {
 // split-K combine by column sums: deep splits with a plain store epilogue
 static bool colsum_combine(const mdemi_gemm_desc* d, const GemmParams& p) {
   return p.split >= 32 && d->batch == 1 && d->alpha == 1.f && d->beta == 0.f && d->bias_mode == MDEMI_BIAS_NONE &&
-         d->act == MDEMI_ACT_NONE && !d->residual && !d->preact && !d->drop_seed && !d->row_scale && d->ldc == d->N;
+         d->act == MDEMI_ACT_NONE && !d->residual && !d->preact && d->ldc == d->N;
 }
 static size_t colsum_combine_bytes(const mdemi_gemm_desc* d, const GemmParams& p) {
   return colsum_combine(d, p) ? colsum_ws_bytes(p.split, (int64_t)d->M * d->N) : 0;

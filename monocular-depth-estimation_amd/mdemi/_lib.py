@@ -65,8 +65,6 @@ class GemmDesc(ctypes.Structure):
         ("batch_inner", i32), ("_pad1", i32),
         ("a_bstride_inner", i64), ("b_bstride_inner", i64), ("c_bstride_inner", i64),
         ("row_scale", vp), ("row_scale_group", i64),
-        ("drop_seed", vp), ("drop_add", ctypes.c_uint64), ("drop_offset", ctypes.c_uint64),
-        ("drop_p", f32), ("_pad2", i32),
     ]
 
 

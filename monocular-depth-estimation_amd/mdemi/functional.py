@@ -108,8 +108,9 @@ def _draw_seed(device):
     return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
 
 
-# Dropout fused into its producer (GEMM epilogues, the attention softmax sweep): the same masks
-# and values as the standalone sweeps, bit for bit; MDEMI_FUSE_DROPOUT=0 keeps the sweeps (A/B).
+# Attention dropout fused into the softmax sweep (the bf16 copy of dropout(P), reused for dV):
+# the same mask and values as the standalone sweeps, bit for bit; MDEMI_FUSE_DROPOUT=0 keeps the
+# sweeps (A/B).  (A dropout stage in the GEMM epilogue was measured and removed: DESIGN.md §5.)
 _FUSE_DROP = [os.environ.get("MDEMI_FUSE_DROPOUT", "1") != "0"]
 
 
@@ -273,8 +274,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
          alpha=1.0, beta=0.0, bias=None, bias_mode=L.BIAS_NONE, act=L.ACT_NONE, aux=None, ldaux=0,
          residual=None, ldres=0, batch=1, a_bstride=0, b_bstride=0, c_bstride=0, aux_bstride=0,
          res_bstride=0, split_k=None, conv=None, preact=None, ldpre=0, pre_bstride=0, rowsum_a=None,
-         a_off=0, b_off=0, c_off=0, inner=None, row_scale=None, row_scale_group=0, a16=None, b16=None, c16=None,
-         drop=None):
+         a_off=0, b_off=0, c_off=0, inner=None, row_scale=None, row_scale_group=0, a16=None, b16=None, c16=None):
     """a_off/b_off/c_off: element offsets into A/B/C (column slices of wider buffers).
     inner=(n, a_bstride_inner, b_bstride_inner, c_bstride_inner): a two-level batch of
     batch = outer * n entries (mdemi_gemm_desc.batch_inner), e.g. (image, head).
@@ -282,9 +282,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
     tensors, same layout; A / B may then be None) and a bf16 copy of C to write -- the bf16
     storage path (mdemi_gemm_bf16x), bit-identical to the fp32-operand bf16 GEMM.  With A (or
     B) None only the bf16 copy exists: B16Unsupported is raised (before any launch) when the
-    bf16 loaders cannot stage this layout.
-    drop=(p, seed, add, offset): inverted dropout fused in the epilogue (mdemi_gemm_desc.drop_seed),
-    the mask _drop(C, p, seed, add, offset) would apply over a contiguous C."""
+    bf16 loaders cannot stage this layout."""
     if inner is not None and inner[0] > 1 and os.environ.get("MDEMI_GEMM_SPLIT_INNER") == "1":
         # debug/A-B path: the same products as one launch per inner index
         n, a2, b2, c2 = inner
@@ -316,9 +314,6 @@ def gemm(A, B, C, M, N, K, *, lda, ldb, ldc, a_layout, b_layout, a_op=L.OP_NONE,
         d.rowsum_a = rowsum_a.data_ptr()
     if row_scale is not None:
         d.row_scale, d.row_scale_group = row_scale.data_ptr(), row_scale_group
-    if drop is not None:
-        d.drop_p, d.drop_add, d.drop_offset = float(drop[0]), int(drop[2]), int(drop[3])
-        d.drop_seed = drop[1].data_ptr()
     lib = L.load()
     need = lib.mdemi_gemm_workspace_size(ctypes.byref(d))
     if need:
@@ -404,11 +399,9 @@ def colsum(x2d, out=None, accumulate=False):
 # --------------------------------------------------------------------------
 
 
-def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NONE, out=None, drop_scale=None,
-                   drop=None):
+def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NONE, out=None, drop_scale=None):
     """drop_scale: per-sample DropPath scale [B] of the product (rows grouped M / B per sample),
-    applied in the epilogue before the residual add; drop: gemm()'s fused dropout (before the
-    residual add)."""
+    applied in the epilogue before the residual add."""
     M, K = x2.shape
     N = weight.shape[0]
     if out is None:
@@ -417,8 +410,7 @@ def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NON
          b_layout=L.L_KCONTIG, a_op=L.OP_GELU if in_gelu else L.OP_NONE,
          bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act,
          residual=residual, ldres=(residual.stride(0) if residual is not None else 0), split_k=1,
-         row_scale=drop_scale, row_scale_group=(M // drop_scale.numel() if drop_scale is not None else 0),
-         drop=drop)
+         row_scale=drop_scale, row_scale_group=(M // drop_scale.numel() if drop_scale is not None else 0))
     return out
 
 
@@ -432,16 +424,12 @@ def _drop_rows(dy2, scale):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, in_gelu, drop_scale, drop):
-        """drop = (p, seed, offset): y = dropout(x W^T + b) (+ residual) with the dropout in the
-        epilogue -- the mask mf.dropout would draw over the product (its seed and offset)."""
+    def forward(ctx, x, weight, bias, residual, in_gelu, drop_scale):
         _require_cuda(x, weight, bias, residual)
         K = x.shape[-1]
         x2 = _c(x).reshape(-1, K)
         res2 = _c(residual).reshape(x2.shape[0], -1) if residual is not None else None
-        out = linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2, drop_scale=drop_scale,
-                             drop=None if drop is None else (drop[0], drop[1], 0, drop[2]))
-        ctx.drop = drop
+        out = linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2, drop_scale=drop_scale)
         ctx.save_for_backward(x2, weight)
         ctx.dx16 = grad_feeds_gemm(x)
         ctx.drop_scale = drop_scale
@@ -459,14 +447,6 @@ class _LinearFn(torch.autograd.Function):
         dy2 = _c(dy).reshape(M, N)
         if ctx.drop_scale is not None:  # the branch's gradient; the residual's stays dy
             dy2 = _drop_rows(dy2, ctx.drop_scale)
-        if ctx.drop is not None:  # the dropout backward: the product's gradient (+ its bf16 copy)
-            p, seed, off = ctx.drop
-            d = torch.empty_like(dy2)
-            d16 = new_b16_like(d) if (d.numel() % 4 == 0 and dy2.data_ptr() % 16 == 0) else None
-            _drop(dy2.data_ptr(), d.data_ptr(), d.numel(), p, seed, offset=off, dst16_ptr=L.ptr(d16))
-            if d16 is not None:
-                set_b16(d, d16)
-            dy2 = d
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, device=dy.device, dtype=torch.float32)
@@ -489,29 +469,23 @@ class _LinearFn(torch.autograd.Function):
         elif want_db:
             colsum(dy2, out=db)
         dres = dy if ctx.has_res and ctx.needs_input_grad[3] else None
-        return dx, dw, db, dres, None, None, None
+        return dx, dw, db, dres, None, None
 
 
 def linear(x, weight, bias=None, residual=None, in_gelu=False, drop_scale=None, p=0.0, training=False):
     """y = (gelu(x) if in_gelu else x) @ W^T + b (+ residual); drop_scale (DropPath, per
     sample [B]): y = residual + drop_scale[sample] * (x @ W^T + b), fused in the epilogue.
     p > 0 and training: y = dropout(x @ W^T + b) (+ residual) -- nn.Dropout on a projection's
-    output before a residual add (luna_layer.py:172-173,250-251, self_attention.py:78-80) --
-    with the dropout in the epilogue (same seed draw, offset and mask as mf.dropout)."""
+    output before a residual add (luna_layer.py:172-173,250-251, self_attention.py:78-80); the
+    residual add is then a separate sweep after the dropout one."""
     if drop_scale is not None and residual is None:
         raise ValueError("linear: drop_scale scales a residual branch and needs residual")
     if training and p > 0.0:
         if drop_scale is not None:
             raise ValueError("linear: dropout and drop_scale together are not supported")
-        if not _FUSE_DROP[0]:
-            y = dropout(_LinearFn.apply(x, weight, bias, None, in_gelu, None, None), p, True)
-            return add(residual, y) if residual is not None else y
-        n = x.numel() // x.shape[-1] * weight.shape[0]
-        seed = _draw_seed(x.device)
-        off = _drop_counter[0]
-        _drop_counter[0] += n
-        return _LinearFn.apply(x, weight, bias, residual, in_gelu, None, (float(p), seed, off))
-    return _LinearFn.apply(x, weight, bias, residual, in_gelu, drop_scale, None)
+        y = dropout(_LinearFn.apply(x, weight, bias, None, in_gelu, None), p, True)
+        return add(residual, y) if residual is not None else y
+    return _LinearFn.apply(x, weight, bias, residual, in_gelu, drop_scale)
 
 
 class _MlpFn(torch.autograd.Function):
@@ -536,20 +510,15 @@ class _MlpFn(torch.autograd.Function):
         h = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
         g = torch.empty(M, Hd, device=x.device, dtype=torch.float32)
         g16 = new_b16_like(g) if g.numel() % 4 == 0 else None  # fc2's operand (bf16 storage)
-        fuse = _FUSE_DROP[0]
-        # fused: g = dropout(act(fc1(x))) and its bf16 copy from fc1's epilogue (same mask)
         gemm(x2, _c(w1), g, M, Hd, K, lda=K, ldb=K, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_KCONTIG,
              bias=b1, bias_mode=L.BIAS_COL if b1 is not None else L.BIAS_NONE, act=act,
-             preact=h, ldpre=Hd, split_k=1, c16=g16 if (p_mid == 0.0 or fuse) else None,
-             drop=(p_mid, seed, 0, 0) if (p_mid > 0.0 and fuse) else None)
-        if p_mid > 0.0 and not fuse:
+             preact=h, ldpre=Hd, split_k=1, c16=g16 if p_mid == 0.0 else None)
+        if p_mid > 0.0:
             _drop(g.data_ptr(), g.data_ptr(), g.numel(), p_mid, seed, dst16_ptr=L.ptr(g16))
         if g16 is not None:
             set_b16(g, g16)
         res2 = _c(residual).reshape(M, N) if residual is not None else None
-        if p_out > 0.0 and fuse:  # out = dropout(fc2(g)) + residual in fc2's epilogue
-            out = linear_fwd_raw(g, _c(w2), b2, residual=res2, drop=(p_out, seed, 1, 0))
-        elif p_out > 0.0:
+        if p_out > 0.0:
             out = linear_fwd_raw(g, _c(w2), b2)
             _drop(out.data_ptr(), out.data_ptr(), out.numel(), p_out, seed, add=1)
             if res2 is not None:
@@ -587,16 +556,15 @@ class _MlpFn(torch.autograd.Function):
         gemm(d2, g, dw2, N, Hd, M, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
              rowsum_a=db2)
         dh = torch.empty(M, Hd, device=dev, dtype=torch.float32)
-        if p_mid > 0.0 and not _FUSE_DROP[0]:
+        if p_mid > 0.0:
             gemm(d2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG)
             _drop(dh.data_ptr(), dh.data_ptr(), dh.numel(), p_mid, seed)
             L.call("mdemi_elementwise", L.EW_ACT_BWD, h.data_ptr(), dh.data_ptr(), dh.data_ptr(), dh.numel(),
                    float(act), 0.0, L.stream())
-        else:  # fused: dh = act'(h) * dropout_bwd(d2 . W2) in the dgrad epilogue (mask of the forward's)
+        else:
             dh16 = new_b16_like(dh)  # the operand of both fc1 gradient GEMMs
             gemm(d2, w2, dh, M, Hd, N, lda=N, ldb=Hd, ldc=Hd, a_layout=L.L_KCONTIG, b_layout=L.L_MNCONTIG,
-                 act=L.ACT_GRAD_OF[act], aux=h, ldaux=Hd, c16=dh16,
-                 drop=(p_mid, seed, 0, 0) if p_mid > 0.0 else None)
+                 act=L.ACT_GRAD_OF[act], aux=h, ldaux=Hd, c16=dh16)
             if dh16 is not None:
                 set_b16(dh, dh16)
         del h, g
@@ -2121,10 +2089,9 @@ class _AttentionFn(torch.autograd.Function):
         dP = torch.empty_like(P)
         if dout is not None:
             dout = _c(dout)
-            fuse = p > 0.0 and _FUSE_DROP[0]  # dP = dropout_bwd(dO . V^T) in the GEMM epilogue
             gemm(dout, vsrc, dP, Sq, Sk, dv, lda=heads * dv, ldb=ldv, ldc=Sk, a_layout=L.L_KCONTIG,
                  b_layout=L.L_KCONTIG, batch=B * heads, a_bstride=Sq * heads * dv, b_bstride=Sk * ldv,
-                 c_bstride=heads * hs, b_off=v_off, inner=(heads, dv, dv, hs), drop=(p, seed, 0, 0) if fuse else None)
+                 c_bstride=heads * hs, b_off=v_off, inner=(heads, dv, dv, hs))
             dvk = dict(lda=Sk, ldb=heads * dv, ldc=ldv, a_layout=L.L_MNCONTIG, b_layout=L.L_MNCONTIG,
                        batch=B * heads, a_bstride=heads * hs, b_bstride=Sq * heads * dv, c_bstride=Sk * ldv,
                        c_off=v_off, inner=(heads, hs, dv, dv), c16=dv16)
@@ -2137,7 +2104,7 @@ class _AttentionFn(torch.autograd.Function):
                 Pd = torch.empty_like(P)
                 _drop(P.data_ptr(), Pd.data_ptr(), P.numel(), p, seed)
                 gemm(Pd, dout, dvv, Sk, dv, Sq, **dvk)
-            if p > 0.0 and not fuse:
+            if p > 0.0:
                 _drop(dP.data_ptr(), dP.data_ptr(), dP.numel(), p, seed)
             if dP_ext is not None:
                 dP_ext = _c(dP_ext)

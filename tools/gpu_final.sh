@@ -15,5 +15,5 @@ python3 -c "
 import json;d=json.loads(open('gpurun_out/${TAG}_bench.json').read().strip().splitlines()[-1])
 print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['cpu_baseline']['value'])
 print('kitti', d['secondary']['images_per_sec'])
-for k,v in d['secondaries'].items(): print(k, v['images_per_sec'], v['ms_per_step'], v['roofline']['bound'], v['roofline']['frac'])"
+for k,v in d['secondaries'].items(): print(k, v.get('images_per_sec', v.get('gpu_images_per_sec')), v.get('ms_per_step'), (v.get('roofline') or {}).get('bound'), (v.get('roofline') or {}).get('frac'))"
 exit $trc
