@@ -372,6 +372,7 @@ class _HbmTimers:
     @staticmethod
     def _wrap(fn, nbytes, nflops, recs):
         def timed(*args):
+            _spin()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(torch.cuda.current_stream())
             rc = fn(*args)
@@ -403,34 +404,71 @@ class _HbmTimers:
         return out or None
 
 
+GEMM_ENTRIES = ("mdemi_gemm_f32", "mdemi_gemm_bf16", "mdemi_gemm_f32e", "mdemi_gemm_bf16x")
+SPIN_CYCLES = 60000  # ~25 us of torch.cuda._sleep ahead of each timed launch
+
+
+def _spin():
+    """Keep the GPU busy while the host enqueues [start event, kernel(s), end event], so the
+    events bracket device time only -- not the host's launch latency of an eager step, which on
+    the configs[4] step's 20-40 us GEMMs is as long as the kernels (round 6: 66 us by events
+    around the Python call vs 37 us in the rocprofv3 trace)."""
+    sleep = getattr(torch.cuda, "_sleep", None)
+    if sleep is not None:
+        sleep(SPIN_CYCLES)
+
+
 def gemm_roofline(trainer, batches):
     """One instrumented (eager, even for a captured trainer) step: HIP events around every
-    libmdemi GEMM launch on its stream; algorithmic FLOPs (2*M*N*K per GEMM) and bytes /
-    measured kernel time, per kernel family."""
+    libmdemi GEMM entry-point call on its stream (the GEMM kernel and, for split K, its slab
+    reduce; not the bf16 casts or bias column sums gemm() may launch first), each preceded by a
+    spin kernel so the events time the device only; algorithmic FLOPs (2*M*N*K per GEMM) and
+    bytes / measured kernel time, per kernel family."""
     from mdemi import functional as mf
-    recs = []
+    from mdemi import _lib as L
+    lib = L.load()
+    recs, pending = [], []
     orig = mf.gemm
+    orig_c = {n: getattr(lib, n) for n in GEMM_ENTRIES}
+
+    def wrap_c(fn):
+        def f(*args):
+            _spin()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(torch.cuda.current_stream())
+            rc = fn(*args)
+            e.record(torch.cuda.current_stream())
+            if pending and pending[-1] is None:
+                pending[-1] = (s, e)
+            return rc
+        return f
 
     def timed(A, B, C, M, N, K, **kw):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record(torch.cuda.current_stream())
-        out = orig(A, B, C, M, N, K, **kw)
-        e.record(torch.cuda.current_stream())
+        pending.append(None)
+        try:
+            out = orig(A, B, C, M, N, K, **kw)
+        finally:
+            ev = pending.pop()
+        if ev is None:
+            return out
         path = mf.LAST_GEMM[0]  # "b16": bf16 operands in HBM (gemm_b16_kernel)
         key = (path, kw.get("a_layout"), kw.get("b_layout"), kw.get("a_op", 0), kw.get("b_op", 0))
         recs.append((key, 2.0 * M * N * K * kw.get("batch", 1),
-                     _gemm_alg_bytes(A, B, M, N, K, kw, ob=2.0 if path == "b16" else 4.0), s, e))
+                     _gemm_alg_bytes(A, B, M, N, K, kw, ob=2.0 if path == "b16" else 4.0), ev[0], ev[1]))
         return out
 
     mf.gemm = timed
-    from mdemi import _lib as L
-    hbm = _HbmTimers(L.load())
+    for n, fn in orig_c.items():
+        setattr(lib, n, wrap_c(fn))
+    hbm = _HbmTimers(lib)
     try:
         with mf.matmul_precision(trainer.precision):
             trainer._eager_step(batches)
         torch.cuda.synchronize()
     finally:
         mf.gemm = orig
+        for n, fn in orig_c.items():
+            setattr(lib, n, fn)
         hbm.restore()
     trainer._hbm_kernels = hbm.summary()
     by = {}
