@@ -33,7 +33,7 @@ def main():
     d = json.loads(line)
     rf = d["roofline"]
     rows = sorted(csv.DictReader(open(f"{tdir}/run_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
-    adam, fam = 0, {}
+    adam, fam, red, last = 0, {}, {}, None
     for r in rows:
         n = r["Kernel_Name"]
         if re.search(r"adamw(_dev)?_kernel", n):
@@ -41,9 +41,16 @@ def main():
             continue
         if adam < warm:
             continue
+        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         f = family_of(n)
         if f:
-            fam.setdefault(f, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            fam.setdefault(f, []).append(dur)
+            red.setdefault(f, []).append(0.0)
+            last = f
+        elif "gemm_splitk_reduce" in n and last is not None:  # inside the same entry-point call
+            red[last][-1] += dur
+        else:
+            last = None
     steps = adam - warm
     key = rf["kernel_regex"]
     t = fam.get(key, [])
@@ -53,10 +60,16 @@ def main():
     print(f"dominant family in the line: {key} ({rf['kernel']}), {len(t) / max(steps, 1):.1f} launches/step")
     if t:
         avg = sum(t) / len(t)
-        print(f"rocprofv3 trace: average {avg:.2f} us per launch -> {rf['flops_per_launch'] / avg / 1e6:.2f} TF/s "
-              f"= {rf['flops_per_launch'] / avg / 1e6 / rf['peak']:.4f} of {rf['peak']}")
+        avg2 = avg + sum(red.get(key, [])) / len(t)
+        if rf["unit"] == "TFLOP/s":
+            rate = lambda us: f"{rf['flops_per_launch'] / us / 1e6:.2f} TF/s = {rf['flops_per_launch'] / us / 1e6 / rf['peak']:.4f} of {rf['peak']}"  # noqa: E731
+        else:
+            rate = lambda us: f"{rf['algorithmic_bytes'] / us / 1e3:.1f} GB/s = {rf['algorithmic_bytes'] / us / 1e3 / rf['peak']:.4f} of {rf['peak']}"  # noqa: E731
+        print(f"rocprofv3 trace: average {avg:.2f} us per GEMM kernel -> {rate(avg)}")
+        print(f"  with the split-K reduce kernels the same entry-point calls launch (what the events "
+              f"bracket): {avg2:.2f} us -> {rate(avg2)}")
     print(f"bench HIP events (same run): {rf['avg_launch_us']} us per launch -> frac {rf['frac']} ({rf['achieved']} "
-          f"TF/s)")
+          f"{rf['unit']})")
     print("families by trace time per step (ms): " + ", ".join(f"{k} {s / max(steps, 1) / 1e3:.2f}" for s, k in tot[:4]))
     if len(tot) > 1:
         print(f"the top two families differ by {100 * (tot[0][0] - tot[1][0]) / tot[0][0]:.1f} % of trace time: "
