@@ -206,6 +206,11 @@ int mdemi_bins_chamfer_bwd(const float* gcent, const float* dloss, float* dedges
 #define MDEMI_WL_DGRAD 2
 int mdemi_conv_weight_layout(const float* w, float* out, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
                              int32_t mode, void* stream);
+/* The same re-layout also writing out16 (optional): the RNE bf16 copy of `out`, the operand a bf16
+ * conv GEMM reads (bf16 storage, configs[4]) -- one sweep instead of the re-layout plus a cast of
+ * the fresh re-laid-out weight every step (layer_utils.py:20-24 ConvBN under torch.autocast). */
+int mdemi_conv_weight_layout16(const float* w, float* out, void* out16, int32_t cout, int32_t cin, int32_t kh,
+                               int32_t kw, int32_t mode, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Sample transform of dataset/depth_dataset.py (replaces DepthDataset.      */

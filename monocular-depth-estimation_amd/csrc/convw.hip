@@ -10,8 +10,10 @@
 
 namespace mdemi {
 
+// out16 (optional): the RNE bf16 copy of each re-laid-out element (a bf16 conv GEMM's operand)
 __global__ void __launch_bounds__(256) conv_wlayout_kernel(const float* __restrict__ w, float* __restrict__ out,
-                                                           int cout, int cin, int kh, int kw, int mode) {
+                                                           __bf16* __restrict__ out16, int cout, int cin, int kh,
+                                                           int kw, int mode) {
   const int64_t n = (int64_t)cout * cin * kh * kw;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = t;
@@ -35,7 +37,9 @@ __global__ void __launch_bounds__(256) conv_wlayout_kernel(const float* __restri
       const int ky = (int)(r / kw);
       src = (((int64_t)co * cin + c) * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx);
     }
-    out[t] = w[src];
+    const float v = w[src];
+    out[t] = v;
+    if (out16) out16[t] = (__bf16)v;
   }
 }
 
@@ -43,14 +47,19 @@ __global__ void __launch_bounds__(256) conv_wlayout_kernel(const float* __restri
 
 using namespace mdemi;
 
-extern "C" int mdemi_conv_weight_layout(const float* w, float* out, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
-                                        int32_t mode, void* stream) {
+extern "C" int mdemi_conv_weight_layout16(const float* w, float* out, void* out16, int32_t cout, int32_t cin,
+                                          int32_t kh, int32_t kw, int32_t mode, void* stream) {
   MDEMI_REQUIRE(w && out && w != out && cout > 0 && cin > 0 && kh > 0 && kw > 0 &&
                     (mode == MDEMI_WL_OHWI || mode == MDEMI_WL_OIHW || mode == MDEMI_WL_DGRAD),
                 "conv_weight_layout: bad args");
   const int64_t n = (int64_t)cout * cin * kh * kw;
   const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
-  hipLaunchKernelGGL(conv_wlayout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, out, cout, cin, kh, kw,
-                     mode);
+  hipLaunchKernelGGL(conv_wlayout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, out, (__bf16*)out16,
+                     cout, cin, kh, kw, mode);
   return check_launch("conv_weight_layout");
+}
+
+extern "C" int mdemi_conv_weight_layout(const float* w, float* out, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
+                                        int32_t mode, void* stream) {
+  return mdemi_conv_weight_layout16(w, out, nullptr, cout, cin, kh, kw, mode, stream);
 }

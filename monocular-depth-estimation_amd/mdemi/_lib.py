@@ -218,6 +218,7 @@ _SIGS = {
     "mdemi_bins_chamfer_fwd": (ctypes.c_int, [vp, vp, i32, i32, i32, i64, f32, vp, vp, vp, vp]),
     "mdemi_bins_chamfer_bwd": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp]),
     "mdemi_conv_weight_layout": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, vp]),
+    "mdemi_conv_weight_layout16": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "mdemi_augment": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32,
                                      f32, f32, vp, vp, vp]),
     "mdemi_window_shuffle": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),

@@ -238,8 +238,8 @@ def new_b16_like(t):
 
 
 # autograd nodes whose backward runs bf16 GEMMs on the gradient of their output
-_GEMM_BWD_NODES = frozenset(("_LinearFnBackward", "_Conv2dFnBackward", "_MlpFnBackward", "_LinearActFnBackward",
-                             "_AttentionFnBackward", "_BatchedGemmFnBackward"))
+_GEMM_BWD_NODES = frozenset(("_LinearFnBackward", "_Conv2dFnBackward", "_Conv2dSkipFnBackward", "_MlpFnBackward",
+                             "_LinearActFnBackward", "_AttentionFnBackward", "_BatchedGemmFnBackward"))
 
 
 def grad_feeds_gemm(x):
@@ -1920,7 +1920,13 @@ def conv_weight_layout(w, mode, conv_shape=None):
         return w.view(cout, cin, 1, 1) if mode == L.WL_OIHW else w.view(cout, 1, 1, cin)
     shape = {L.WL_OHWI: (cout, kh, kw, cin), L.WL_OIHW: (cout, cin, kh, kw), L.WL_DGRAD: (kh, kw, cout, cin)}[mode]
     out = torch.empty(shape, device=w.device, dtype=torch.float32)
-    L.call("mdemi_conv_weight_layout", w.data_ptr(), out.data_ptr(), cout, cin, kh, kw, mode, L.stream())
+    # a GEMM operand (forward / input-gradient layouts) under bf16 storage: its bf16 copy in the
+    # same sweep, instead of a cast of the fresh re-laid-out weight by the GEMM
+    out16 = new_b16_like(out) if mode != L.WL_OIHW else None
+    L.call("mdemi_conv_weight_layout16", w.data_ptr(), out.data_ptr(), L.ptr(out16), cout, cin, kh, kw, mode,
+           L.stream())
+    if out16 is not None:
+        set_b16(out, out16)
     return out
 
 

@@ -45,7 +45,7 @@ def main():
 
         def wrapped(*args, _fn=fn, _name=name):  # noqa: E306
             stack = [f for f in traceback.extract_stack()[:-1] if "/mdemi/" in f.filename]
-            inner = [f for f in stack if not f.filename.endswith(("_lib.py",))][-2:]
+            inner = [f for f in stack if not f.filename.endswith(("_lib.py",))][-4:]
             outer = [f for f in stack if not f.filename.endswith(("_lib.py", "functional.py"))][-2:]
             where = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in (inner + outer)[::-1])
             counts[(_name, where)] += 1
