@@ -399,9 +399,10 @@ def colsum(x2d, out=None, accumulate=False):
 # --------------------------------------------------------------------------
 
 
-def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NONE, out=None, drop_scale=None):
+def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NONE, out=None, drop_scale=None,
+                   c16=None):
     """drop_scale: per-sample DropPath scale [B] of the product (rows grouped M / B per sample),
-    applied in the epilogue before the residual add."""
+    applied in the epilogue before the residual add; c16: the output's bf16 copy (gemm())."""
     M, K = x2.shape
     N = weight.shape[0]
     if out is None:
@@ -410,7 +411,8 @@ def linear_fwd_raw(x2, weight, bias, in_gelu=False, residual=None, act=L.ACT_NON
          b_layout=L.L_KCONTIG, a_op=L.OP_GELU if in_gelu else L.OP_NONE,
          bias=bias, bias_mode=L.BIAS_COL if bias is not None else L.BIAS_NONE, act=act,
          residual=residual, ldres=(residual.stride(0) if residual is not None else 0), split_k=1,
-         row_scale=drop_scale, row_scale_group=(M // drop_scale.numel() if drop_scale is not None else 0))
+         row_scale=drop_scale, row_scale_group=(M // drop_scale.numel() if drop_scale is not None else 0),
+         c16=c16)
     return out
 
 
@@ -424,12 +426,16 @@ def _drop_rows(dy2, scale):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, in_gelu, drop_scale):
+    def forward(ctx, x, weight, bias, residual, in_gelu, drop_scale, out_b16=False):
         _require_cuda(x, weight, bias, residual)
         K = x.shape[-1]
         x2 = _c(x).reshape(-1, K)
         res2 = _c(residual).reshape(x2.shape[0], -1) if residual is not None else None
-        out = linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2, drop_scale=drop_scale)
+        out = torch.empty(x2.shape[0], weight.shape[0], device=x.device, dtype=torch.float32)
+        o16 = new_b16_like(out) if out_b16 else None  # the output feeds bf16 GEMMs (attention products)
+        linear_fwd_raw(x2, _c(weight), bias, in_gelu=in_gelu, residual=res2, drop_scale=drop_scale, out=out, c16=o16)
+        if o16 is not None:
+            set_b16(out, o16)
         ctx.save_for_backward(x2, weight)
         ctx.dx16 = grad_feeds_gemm(x)
         ctx.drop_scale = drop_scale
@@ -469,23 +475,25 @@ class _LinearFn(torch.autograd.Function):
         elif want_db:
             colsum(dy2, out=db)
         dres = dy if ctx.has_res and ctx.needs_input_grad[3] else None
-        return dx, dw, db, dres, None, None
+        return dx, dw, db, dres, None, None, None
 
 
-def linear(x, weight, bias=None, residual=None, in_gelu=False, drop_scale=None, p=0.0, training=False):
+def linear(x, weight, bias=None, residual=None, in_gelu=False, drop_scale=None, p=0.0, training=False,
+           out_b16=False):
     """y = (gelu(x) if in_gelu else x) @ W^T + b (+ residual); drop_scale (DropPath, per
     sample [B]): y = residual + drop_scale[sample] * (x @ W^T + b), fused in the epilogue.
     p > 0 and training: y = dropout(x @ W^T + b) (+ residual) -- nn.Dropout on a projection's
     output before a residual add (luna_layer.py:172-173,250-251, self_attention.py:78-80); the
-    residual add is then a separate sweep after the dropout one."""
+    residual add is then a separate sweep after the dropout one.  out_b16 (no dropout): the
+    output's bf16 copy from the epilogue, for bf16 GEMMs that read it (bf16 storage)."""
     if drop_scale is not None and residual is None:
         raise ValueError("linear: drop_scale scales a residual branch and needs residual")
     if training and p > 0.0:
         if drop_scale is not None:
             raise ValueError("linear: dropout and drop_scale together are not supported")
-        y = dropout(_LinearFn.apply(x, weight, bias, None, in_gelu, None), p, True)
+        y = dropout(_LinearFn.apply(x, weight, bias, None, in_gelu, None, False), p, True)
         return add(residual, y) if residual is not None else y
-    return _LinearFn.apply(x, weight, bias, residual, in_gelu, drop_scale)
+    return _LinearFn.apply(x, weight, bias, residual, in_gelu, drop_scale, out_b16)
 
 
 class _MlpFn(torch.autograd.Function):

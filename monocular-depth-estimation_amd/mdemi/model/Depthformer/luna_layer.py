@@ -50,10 +50,11 @@ class PreNormLunaBlock(nn.Module):
         aux_n, aux = mf.layer_norm_skip(aux, self.aux_norm.weight, self.aux_norm.bias, self.aux_norm.eps,
                                         out_b16=True)
         hidden_n, hidden = mf.layer_norm_skip(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
-        q1 = mf.linear(aux_n, self.q1_proj.weight, self.q1_proj.bias)                       # (B*K, qk)
+        # q/k/v projections feed the attention GEMMs: their bf16 copies from the epilogues
+        q1 = mf.linear(aux_n, self.q1_proj.weight, self.q1_proj.bias, out_b16=True)         # (B*K, qk)
         w_h = torch.cat([self.k1_proj.weight, self.v1_proj.weight, self.q2_proj.weight])
         b_h = torch.cat([self.k1_proj.bias, self.v1_proj.bias, self.q2_proj.bias])
-        kvq = mf.linear(hidden_n, w_h, b_h)                                                  # (B*HW, qk+d+qk)
+        kvq = mf.linear(hidden_n, w_h, b_h, out_b16=True)                                    # (B*HW, qk+d+qk)
         out1, attn1 = mf.attention(q1, kvq, kvq, B, K, HW, nh, qk // nh, d // nh, self.attn_scale, q_off=0,
                                    k_off=0, v_off=qk, p=self.attn_drop.p, training=tr, out_b16=True)
         out1 = mf.linear(out1, self.o1_proj.weight, self.o1_proj.bias, p=self.drop.p, training=tr)  # (B*K, a)
@@ -62,7 +63,7 @@ class PreNormLunaBlock(nn.Module):
                                   out_b16=True)
         w_a = torch.cat([self.k2_proj.weight, self.v2_proj.weight])
         b_a = torch.cat([self.k2_proj.bias, self.v2_proj.bias])
-        kv2 = mf.linear(out_n, w_a, b_a)                                                     # (B*K, qk+d)
+        kv2 = mf.linear(out_n, w_a, b_a, out_b16=True)                                       # (B*K, qk+d)
         out2, attn2 = mf.attention(kvq, kv2, kv2, B, HW, K, nh, qk // nh, d // nh, self.attn_scale,
                                    q_off=qk + d, k_off=0, v_off=qk, p=self.attn_drop.p, training=tr, out_b16=True)
         # hidden + dropout(o2_proj(out2)): the dropout and the residual add in the projection's epilogue

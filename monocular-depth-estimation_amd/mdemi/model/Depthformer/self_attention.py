@@ -34,7 +34,7 @@ class SelfAttentionBlock(nn.Module):
         h, hidden = mf.layer_norm_skip(hidden, self.norm.weight, self.norm.bias, self.norm.eps, out_b16=True)
         w = torch.cat([self.query_proj.weight, self.key_proj.weight, self.value_proj.weight])
         b = torch.cat([self.query_proj.bias, self.key_proj.bias, self.value_proj.bias])
-        qkv = mf.linear(h, w, b)
+        qkv = mf.linear(h, w, b, out_b16=True)  # the attention GEMMs' operand: bf16 copy from the epilogue
         o, attn = mf.attention(qkv, qkv, qkv, B, S, S, nh, kq // nh, d // nh, self.attn_scale, q_off=0, k_off=kq,
                                v_off=2 * kq, p=self.attn_drop.p, training=self.training, out_b16=True)
         # hidden + dropout(out_proj(o)): dropout and residual add in the projection's epilogue
